@@ -1,0 +1,147 @@
+"""Flagship benchmark: FFN-stack training throughput (whole-node tokens/s) on MI355X.
+
+Metric/config from BASELINE.json: "FFN tokens/sec (whole node) at hidden=4096 for DDP/FSDP/MP, 1/2/4/8
+MI355X" on the 8-layer hidden=4096 FFN stack (FFN = 4·hidden = 16384, ReLU, as train_ffns.py:361),
+batch 8 × seq 1024 = 8192 tokens per rank per step, bf16 compute with fp32 master weights, SGD (the
+reference optimizer, train_ffns.py:172), random-init weights and synthetic device-generated data.
+
+    python bench.py --gpus N --steps K --warmup W            # N=1 in-process
+    torchrun --nproc-per-node N bench.py --gpus N ...          # one rank per GPU over RCCL/xGMI
+
+Each timed step is the full training step: device mock-data generation, forward, backward (all weight
+and input gradients except the unused layer-0 input grad), gradient communication and the optimizer
+update.  K steps are bracketed by cuda synchronize + barrier on both sides; the max over ranks is
+reported; rank 0 prints ONE JSON line.  Weak scaling: every rank processes 8192 tokens per step under
+DDP/FSDP (global batch = 8·N sequences); ``--method tp`` shards each layer over the GPUs instead
+(tokens per step fixed: strong scaling).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+import dllm  # noqa: F401
+from dllm.parallel import comm
+from dllm.parallel.engine import FFNTrainer
+from dllm.parallel.mesh import Mesh, init_distributed
+from dllm.utils.config import ModelConfig, TrainConfig
+from dllm.utils.data import DeviceMockData
+from dllm.utils.metrics import flops_per_step
+
+METRIC = "FFN tokens/sec (whole node) at hidden=4096 for DDP/FSDP/MP, 1/2/4/8 MI355X"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=0)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--method", choices=["ddp", "fsdp", "tp", "hybrid"], default="ddp")
+    p.add_argument("--tp", type=int, default=0, help="TP degree for --method hybrid")
+    p.add_argument("--model_size", type=int, default=4096)
+    p.add_argument("--ffn_dim", type=int, default=0)
+    p.add_argument("--layers", type=int, default=8)
+    p.add_argument("--batch_size", type=int, default=8)
+    p.add_argument("--seq_len", type=int, default=1024)
+    p.add_argument("--act", default="relu")
+    p.add_argument("--gated", action="store_true")
+    p.add_argument("--dtype", default="bf16")
+    p.add_argument("--grad_dtype", default="fp32")
+    p.add_argument("--optimizer", default="sgd")
+    p.add_argument("--bucket_mb", type=float, default=0.0)
+    p.add_argument("--recompute", default="none")
+    p.add_argument("--sequence_parallel", action="store_true")
+    p.add_argument("--seed", type=int, default=1234)
+    p.add_argument("--json_out", default="")
+    return p.parse_args()
+
+
+def main() -> int:
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    n = a.gpus or world
+    if n != world:
+        raise SystemExit(f"--gpus {n} but WORLD_SIZE={world}: launch N>1 with torchrun")
+    if world > 1:
+        init_distributed("nccl")
+    else:
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    if a.method == "ddp":
+        dp_mode, dp, tp = "ddp", n, 1
+    elif a.method == "fsdp":
+        dp_mode, dp, tp = "fsdp", n, 1
+    elif a.method == "tp":
+        dp_mode, dp, tp = "none", 1, n
+    else:
+        tp = a.tp or min(n, 2)
+        dp_mode, dp = "fsdp", n // tp
+    m = ModelConfig(model_size=a.model_size, ffn_dim=a.ffn_dim, layers=a.layers, act=a.act, gated=a.gated)
+    cfg = TrainConfig(model=m, batch_size=a.batch_size, seq_len=a.seq_len, num_steps=a.steps, dtype=a.dtype,
+                      grad_dtype=a.grad_dtype, optimizer=a.optimizer, dp_mode=dp_mode, dp=dp, tp=tp,
+                      bucket_mb=a.bucket_mb, recompute=a.recompute, sequence_parallel=a.sequence_parallel,
+                      data="device")
+    mesh = Mesh.build(dp, tp)
+    eng = FFNTrainer(cfg, mesh, dev)
+    from dllm.models.ffn import init_ffn_params_device
+
+    eng.load_full_params(init_ffn_params_device(m.D, m.F, m.layers, a.seed, dev, m.gated))
+    torch.cuda.synchronize()
+    data = DeviceMockData(cfg.tokens, m.D, cfg.torch_dtype, dev)
+    seed_base = 10_000 * (mesh.dp_rank + 1)
+
+    for i in range(a.warmup):
+        x, dy = data.fill(seed_base + i)
+        eng.train_step(x, dy)
+    torch.cuda.synchronize()
+    comm.barrier(device=dev)
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        x, dy = data.fill(seed_base + a.warmup + i)
+        eng.train_step(x, dy)
+    torch.cuda.synchronize()
+    comm.barrier(device=dev)
+    el = time.perf_counter() - t0
+    if world > 1:
+        import torch.distributed as dist
+
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    ms = el / a.steps * 1e3
+    tokens_global = cfg.tokens * dp
+    value = tokens_global * a.steps / el
+    tflops = flops_per_step(cfg, tp=tp, recompute=cfg.recompute) / (ms / 1e3) / 1e12
+    finite = bool(torch.isfinite(eng.master[:1024]).all().item())
+    par = {"ddp": f"dp{n}", "fsdp": f"fsdp{n}", "tp": f"tp{n}", "hybrid": f"fsdp{dp}xtp{tp}"}[a.method]
+    rec = {
+        "metric": METRIC, "value": round(value, 1), "unit": "tokens/s", "n_gpus": n, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
+        "scaling": "strong" if a.method == "tp" else "weak", "vs_baseline": None, "dtype": a.dtype,
+        "data": "synthetic (device Philox N(0,1) x, 0.1*N(0,1) dloss/dx; random-init weights)",
+        "config": {"model": f"ffn-stack L{m.layers} D{m.D} F{m.F} {'swiglu-' if m.gated else ''}{m.act}",
+                   "global_batch": a.batch_size * dp, "seq_len": a.seq_len, "parallelism": par,
+                   "optimizer": a.optimizer, "grad_dtype": a.grad_dtype, "master_weights": "fp32"},
+        "tflops_per_gpu": round(tflops, 1), "finite": finite,
+    }
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                json.dump(rec, f)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,12 @@
+"""MI355X-native distributed FFN training (DDP / FSDP / TP-MP / hybrid) — gfx950 HIP kernels + RCCL.
+
+A from-scratch re-design of martin-kukla/distributed-llm-code-samples (``train_ffns.py``) for AMD
+Instinct MI355X: explicit forward/backward of Transformer FFN stacks on hand-written CDNA4 MFMA GEMMs
+with fused epilogues, fused optimizers, device-side mock data, and data / fully-sharded / tensor
+parallelism over RCCL (xGMI) with one communicator + stream per communication role.
+
+Importable as ``dllm`` (see ``dllm.py`` at the repository root).
+"""
+__version__ = "0.1.0"
+
+from .utils.config import ModelConfig, TrainConfig  # noqa: F401

@@ -1,0 +1,80 @@
+// Shared device/host helpers for the gfx950 (CDNA4, MI355X) kernels of this framework.
+// Written directly for CDNA4: 64-lane waves, MFMA, LDS-DMA (global_load_lds), no CUDA shims.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dllm {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4_t;
+typedef __attribute__((ext_vector_type(4))) short s16x4_t;
+typedef __attribute__((ext_vector_type(8))) short s16x8_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+
+#define DLLM_LDS __attribute__((address_space(3)))
+#define DLLM_GLB __attribute__((address_space(1)))
+
+// ---- dtype / enum codes shared with the Python side (ops/_native.py) ----
+enum DType : int { DT_BF16 = 0, DT_F32 = 1 };
+enum Layout : int { L_NT = 0, L_NN = 1, L_TN = 2 };
+// Epilogues fused into the GEMM (reference ops they replace: train_ffns.py:42,45,48,51).
+//   EPI_STORE : C = alpha*acc (+ beta*C)                       plain linear fwd / dgrad / wgrad
+//   EPI_ACT   : C = act(acc); aux_out = acc (pre-activation)  linear + activation fwd (K1+K2)
+//   EPI_DACT  : C = acc * act'(aux)                            dgrad + activation bwd mask (K5+K6)
+//   EPI_GLU   : gated: acc tiles of W1/W3 interleaved by 16 rows; C = act(h1)*h3; aux_out = [h1|h3]
+//   EPI_DGLU  : gated bwd: C(16-col interleaved [dh1|dh3]) from acc = da and aux = interleaved [h1|h3]
+enum Epi : int { EPI_STORE = 0, EPI_ACT = 1, EPI_DACT = 2, EPI_GLU = 3, EPI_DGLU = 4 };
+enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_SILU = 2, ACT_GELU = 3 };
+
+__device__ __forceinline__ float bf2f(uint16_t v) {
+  return __uint_as_float(((uint32_t)v) << 16);
+}
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  // plain cast -> v_cvt_pk_bf16_f32 (RNE, NaN-preserving) on gfx950
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(uint16_t, b);
+}
+
+__device__ __forceinline__ float act_fwd(int act, float x) {
+  switch (act) {
+    case ACT_RELU: return x > 0.f ? x : 0.f;
+    case ACT_SILU: return x / (1.f + __expf(-x));
+    case ACT_GELU: {  // tanh approximation (torch gelu(approximate='tanh'))
+      const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+      float u = k0 * (x + k1 * x * x * x);
+      return 0.5f * x * (1.f + tanhf(u));
+    }
+    default: return x;
+  }
+}
+// derivative d act / d x evaluated at pre-activation x
+__device__ __forceinline__ float act_grad(int act, float x) {
+  switch (act) {
+    case ACT_RELU: return x > 0.f ? 1.f : 0.f;
+    case ACT_SILU: {
+      float s = 1.f / (1.f + __expf(-x));
+      return s * (1.f + x * (1.f - s));
+    }
+    case ACT_GELU: {
+      const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+      float x2 = x * x;
+      float u = k0 * (x + k1 * x2 * x);
+      float t = tanhf(u);
+      return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
+    }
+    default: return 1.f;
+  }
+}
+
+// Bijective XCD-aware remap of a linear block id (cdna_hip_programming.md §5, T1): blocks that the
+// dispatcher deals round-robin to the 8 XCDs get contiguous ranges of logical ids, so tiles that
+// share operand panels run on one XCD and hit its private L2.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int nx = 8;
+  int xcd = bid % nx, q = nwg / nx, r = nwg % nx;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / nx;
+}
+
+}  // namespace dllm

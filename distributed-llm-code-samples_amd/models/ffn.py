@@ -1,0 +1,133 @@
+"""Transformer FFN sub-block stack with explicit ("first principles") forward and backward.
+
+Reference semantics (train_ffns.py:35-94):
+
+* parameters ``W1 [F, D]``, ``W2 [D, F]`` in ``[out, in]`` layout, ``scale·randn`` with scale 2e-2,
+  drawn W1 then W2, layer by layer, after the step seeds (``:35-39``, ``:360-361``);
+* ``y = act(x·W1ᵀ)·W2ᵀ`` — no bias, no residual, no norm (``:54-58``);
+* backward by hand: ``dW2 = dyᵀ·a``, ``da = (dy·W2)⊙act'(h)``, ``dW1 = daᵀ·x``, ``dx = da·W1``
+  (``:61-70``); the reference recomputes ``h`` from the saved layer input (``recompute="full"`` here).
+
+MI355X design: each layer is 4 GEMMs in forward+backward order ``fwd1, fwd2 | dW2, da, dx, dW1``, every
+elementwise op fused into a GEMM epilogue (activation into fwd1, activation-derivative mask into the
+``da`` dgrad), so the only HBM traffic is GEMM operands.  With ``recompute="none"`` (default) the forward
+keeps ``a`` (and ``h`` for non-ReLU activations) so the backward runs 4 GEMMs instead of the reference's
+5 — 6·P·T model FLOPs instead of 7·P·T.  ReLU needs no ``h``: ``act'(h) = [a > 0]``.
+
+Gated (SwiGLU, Llama-3 FFN): ``a = act(x·W1ᵀ) ⊙ (x·W3ᵀ)``.  W1 and W3 are stored row-interleaved in
+16-row blocks as one ``W13 [2F, D]`` so a single GEMM produces both pre-activations and its epilogue
+combines each gate/up pair inside one lane (``epi="glu"``); the backward ``epi="dglu"`` writes the
+interleaved ``[dg|du]`` that feeds one dgrad and one wgrad GEMM against W13.
+"""
+from __future__ import annotations
+
+import torch
+
+from ..ops.gemm import gemm
+from ..utils.config import INIT_SCALE
+
+GLU_BLOCK = 16
+
+
+# --------------------------------------------------------------------------------------------------
+# parameter init
+# --------------------------------------------------------------------------------------------------
+def init_linear_layer(m: int, n: int, gen: torch.Generator | None, scale: float = INIT_SCALE) -> torch.Tensor:
+    """``[n, m]`` weight (``[out, in]``), reference init (train_ffns.py:35-36)."""
+    return scale * torch.randn((n, m), generator=gen)
+
+
+def init_ffn_layer(D: int, F: int, gen: torch.Generator | None, gated: bool = False) -> dict:
+    """One layer's logical parameters in the reference RNG order (W1 then W2; W3 last if gated)."""
+    p = {"w1": init_linear_layer(D, F, gen), "w2": init_linear_layer(F, D, gen)}
+    if gated:
+        p["w3"] = init_linear_layer(D, F, gen)
+    return p
+
+
+def init_ffn_params_device(D: int, F: int, L: int, seed: int, device, gated: bool = False,
+                           scale: float = INIT_SCALE) -> list[dict]:
+    """Device-side init (Philox, one stream per (layer, matrix)); identical on every rank and on CPU."""
+    from ..ops.elementwise import rng_normal_
+
+    out = []
+    for l in range(L):
+        p = {}
+        for j, (name, shape) in enumerate((("w1", (F, D)), ("w2", (D, F)), ("w3", (F, D)))):
+            if name == "w3" and not gated:
+                continue
+            t = torch.empty(shape, dtype=torch.float32, device=device)
+            rng_normal_(t, seed=seed, stream_id=1000 + 4 * l + j, scale=scale)
+            p[name] = t
+        out.append(p)
+    return out
+
+
+def interleave_w13(w1: torch.Tensor, w3: torch.Tensor) -> torch.Tensor:
+    """[F,D],[F,D] -> [2F,D] with 16-row blocks alternating W1, W3."""
+    F, D = w1.shape
+    if F % GLU_BLOCK:
+        raise ValueError(f"gated FFN needs F % {GLU_BLOCK} == 0 (F={F})")
+    return torch.stack([w1.reshape(F // GLU_BLOCK, GLU_BLOCK, D), w3.reshape(F // GLU_BLOCK, GLU_BLOCK, D)],
+                       dim=1).reshape(2 * F, D)
+
+
+def deinterleave_w13(w13: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    R, D = w13.shape
+    v = w13.reshape(R // (2 * GLU_BLOCK), 2, GLU_BLOCK, D)
+    return v[:, 0].reshape(R // 2, D), v[:, 1].reshape(R // 2, D)
+
+
+# --------------------------------------------------------------------------------------------------
+# one layer
+# --------------------------------------------------------------------------------------------------
+def needs_preact(act: str, gated: bool) -> bool:
+    """Whether the backward needs the pre-activation h (ReLU recovers act' from a itself)."""
+    return gated or act != "relu"
+
+
+def layer_fwd(x: torch.Tensor, w1: torch.Tensor, w2: torch.Tensor, act: str, gated: bool,
+              a_out: torch.Tensor, h_out: torch.Tensor | None, y_out: torch.Tensor) -> torch.Tensor:
+    """y = act(x·W1ᵀ)·W2ᵀ  (gated: (act(x·W1ᵀ)⊙x·W3ᵀ)·W2ᵀ with ``w1`` = interleaved W13)."""
+    if gated:
+        gemm(x, w1, "nt", out=a_out, epi="glu", act=act, aux_out=h_out)
+    else:
+        gemm(x, w1, "nt", out=a_out, epi="act", act=act, aux_out=h_out)
+    gemm(a_out, w2, "nt", out=y_out)
+    return y_out
+
+
+def layer_bwd(dy: torch.Tensor, x: torch.Tensor, w1: torch.Tensor, w2: torch.Tensor, act: str, gated: bool,
+              a: torch.Tensor, h: torch.Tensor | None, gw1: torch.Tensor, gw2: torch.Tensor,
+              da_buf: torch.Tensor, dx_out: torch.Tensor | None, hooks=None) -> torch.Tensor | None:
+    """Backward of one layer; writes weight grads into ``gw1``/``gw2`` (overwrite) and returns dx.
+
+    Order ``dW2, da, dx, dW1`` so that (a) the W2 gradient is ready for its collective first and (b) a
+    TP input-grad all-reduce of ``dx`` overlaps the dW1 GEMM.  ``hooks`` may define ``after_w2``,
+    ``after_dx`` and ``after_w1`` callbacks (communication issue points).
+    """
+    gemm(dy, a, "tn", out=gw2)                                        # dW2 = dyᵀ·a        [D, F]
+    if hooks is not None:
+        hooks.after_w2()
+    if gated:
+        gemm(dy, w2, "nn", out=da_buf, epi="dglu", act=act, aux=h)    # [dg|du] interleaved [T, 2F]
+    else:
+        gemm(dy, w2, "nn", out=da_buf, epi="dact", act=act, aux=h if h is not None else a)
+    dx = None
+    if dx_out is not None:
+        dx = gemm(da_buf, w1, "nn", out=dx_out)                       # dx = da·W1         [T, D]
+        if hooks is not None:
+            hooks.after_dx(dx)
+    gemm(da_buf, x, "tn", out=gw1)                                    # dW1 = daᵀ·x        [F, D]
+    if hooks is not None:
+        hooks.after_w1()
+    return dx
+
+
+def recompute_fwd1(x: torch.Tensor, w1: torch.Tensor, act: str, gated: bool, a_out: torch.Tensor,
+                   h_out: torch.Tensor | None) -> None:
+    """Reference-style activation recompute (train_ffns.py:63,66) for ``recompute='full'``."""
+    if gated:
+        gemm(x, w1, "nt", out=a_out, epi="glu", act=act, aux_out=h_out)
+    else:
+        gemm(x, w1, "nt", out=a_out, epi="act", act=act, aux_out=h_out)

@@ -1,0 +1,128 @@
+"""Device RNG, fused optimizer steps and casts (native on HIP tensors, torch reference on CPU)."""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .. import _native
+
+# Philox stream separation for the mock data of one step (x and dloss_dx, train_ffns.py:149-150)
+STREAM_X, STREAM_DY = 0, 1
+
+
+def rng_normal_(out: torch.Tensor, seed: int, stream_id: int = 0, scale: float = 1.0) -> torch.Tensor:
+    """Fill ``out`` with ``scale·N(0,1)``, deterministic in (seed, stream_id, numel) on any device.
+
+    GPU: Philox4x32-10 kernel.  CPU: the same Philox stream computed in torch (bitwise-identical
+    uniform draws; normals equal up to libm differences), so CPU tests and GPU runs see the same data.
+    """
+    if not out.is_contiguous():
+        raise ValueError("rng_normal_ needs a contiguous tensor")
+    n = out.numel()
+    if out.device.type == "cuda":
+        rc = _native.lib().dllm_rng_normal(out.data_ptr(), _native.dtype_code(out.dtype), n, seed & (2**64 - 1),
+                                           stream_id & (2**64 - 1), float(scale), _native.stream_ptr(out.device))
+        _native.check(rc, "dllm_rng_normal")
+        return out
+    out.copy_(_philox_normal_cpu(n, seed, stream_id, scale).view(out.shape))
+    return out
+
+
+def _mulhilo(a: int, b: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    p = b.to(torch.int64) * a  # < 2^64, fits as unsigned; use int64 with masking
+    lo = p & 0xFFFFFFFF
+    hi = (p >> 32) & 0xFFFFFFFF
+    return hi, lo
+
+
+def _philox_normal_cpu(n: int, seed: int, stream_id: int, scale: float) -> torch.Tensor:
+    n4 = (n + 3) // 4
+    idx = torch.arange(n4, dtype=torch.int64)
+    c0 = idx & 0xFFFFFFFF
+    c1 = (idx >> 32) & 0xFFFFFFFF
+    c2 = torch.full_like(idx, stream_id & 0xFFFFFFFF)
+    c3 = torch.full_like(idx, (stream_id >> 32) & 0xFFFFFFFF)
+    k0, k1 = seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF
+    M0, M1, W0, W1 = 0xD2511F53, 0xCD9E8D57, 0x9E3779B9, 0xBB67AE85
+    for _ in range(10):
+        hi0, lo0 = _mulhilo(M0, c0)
+        hi1, lo1 = _mulhilo(M1, c2)
+        c0, c1, c2, c3 = hi1 ^ c1 ^ k0, lo1, hi0 ^ c3 ^ k1, lo0
+        k0 = (k0 + W0) & 0xFFFFFFFF
+        k1 = (k1 + W1) & 0xFFFFFFFF
+    inv = 2.3283064365386963e-10
+
+    def bm(a, b):
+        u1 = (a.to(torch.float32) + 1.0) * inv
+        u2 = b.to(torch.float32) * inv
+        r = torch.sqrt(-2.0 * torch.log(u1))
+        th = 2 * math.pi * u2
+        return r * torch.cos(th), r * torch.sin(th)
+
+    z0, z1 = bm(c0, c1)
+    z2, z3 = bm(c2, c3)
+    z = torch.stack([z0, z1, z2, z3], dim=1).reshape(-1)[:n]
+    return z * scale
+
+
+def _grad_code(g: torch.Tensor) -> int:
+    return _native.dtype_code(g.dtype)
+
+
+def sgd_step_(master: torch.Tensor, grad: torch.Tensor, lr: float, copy: torch.Tensor | None = None,
+              grad_scale: float = 1.0) -> None:
+    """``master += (-lr)·grad`` in place (reference ``param.add_(-LR*grad)``), then ``copy = bf16(master)``."""
+    if master.dtype != torch.float32:
+        raise TypeError("master weights must be fp32")
+    if master.device.type == "cuda":
+        n = master.numel()
+        if n % 4 == 0 and master.is_contiguous() and grad.is_contiguous():
+            rc = _native.lib().dllm_sgd_step(master.data_ptr(), grad.data_ptr(), _grad_code(grad),
+                                             copy.data_ptr() if copy is not None else None, n, float(lr),
+                                             float(grad_scale), _native.stream_ptr(master.device))
+            _native.check(rc, "dllm_sgd_step")
+            return
+        raise ValueError("sgd_step_ on GPU needs contiguous buffers with numel % 4 == 0")
+    g = grad.float()
+    if grad_scale != 1.0:
+        g = g * grad_scale
+    master.add_(-lr * g)
+    if copy is not None:
+        copy.copy_(master)
+
+
+def adam_step_(master: torch.Tensor, grad: torch.Tensor, m: torch.Tensor, v: torch.Tensor, step: int, lr: float,
+               b1: float = 0.9, b2: float = 0.95, eps: float = 1e-8, wd: float = 0.0,
+               copy: torch.Tensor | None = None, grad_scale: float = 1.0) -> None:
+    """Fused AdamW on flat fp32 buffers (decoupled weight decay)."""
+    if master.device.type == "cuda":
+        n = master.numel()
+        if n % 4:
+            raise ValueError("adam_step_ on GPU needs numel % 4 == 0")
+        rc = _native.lib().dllm_adam_step(master.data_ptr(), grad.data_ptr(), _grad_code(grad), m.data_ptr(),
+                                          v.data_ptr(), copy.data_ptr() if copy is not None else None, n,
+                                          float(lr), float(b1), float(b2), float(eps), float(wd), int(step),
+                                          float(grad_scale), _native.stream_ptr(master.device))
+        _native.check(rc, "dllm_adam_step")
+        return
+    g = grad.float() * grad_scale
+    m.mul_(b1).add_((1 - b1) * g)
+    v.mul_(b2).add_((1 - b2) * g * g)
+    bc1, bc2 = 1 - b1 ** step, 1 - b2 ** step
+    upd = (m / bc1) / (torch.sqrt(v / bc2) + eps) + wd * master
+    master.sub_(lr * upd)
+    if copy is not None:
+        copy.copy_(master)
+
+
+def cast_(src: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:
+    if src.numel() != dst.numel():
+        raise ValueError("cast_: size mismatch")
+    if src.device.type == "cuda" and src.dtype != dst.dtype and src.is_contiguous() and dst.is_contiguous():
+        rc = _native.lib().dllm_cast(src.data_ptr(), _native.dtype_code(src.dtype), dst.data_ptr(),
+                                     _native.dtype_code(dst.dtype), src.numel(), _native.stream_ptr(src.device))
+        _native.check(rc, "dllm_cast")
+        return dst
+    dst.copy_(src.view(dst.shape) if src.shape != dst.shape else src)
+    return dst

@@ -1,0 +1,150 @@
+"""GEMM op with fused FFN epilogues.
+
+``gemm(a, b, layout, ...)`` computes, with fp32 accumulation,
+
+* ``"nt"``: ``C[M,N] = A[M,K] · B[N,K]ᵀ``   (linear forward, reference ``linear_fwd`` train_ffns.py:41-42)
+* ``"nn"``: ``C[M,N] = A[M,K] · B[K,N]``    (input gradient, ``einsum('bc,cd->bd')`` train_ffns.py:45)
+* ``"tn"``: ``C[M,N] = A[K,M]ᵀ · B[K,N]``   (weight gradient, ``einsum('bc,bd->cd')`` train_ffns.py:45)
+
+followed by an epilogue:
+
+* ``"store"``: ``C = alpha·acc + beta·C``
+* ``"act"``:   ``C = act(acc)``; ``aux_out = acc`` if given (pre-activation kept for the backward)
+* ``"dact"``:  ``C = acc · act'(aux)``  (``aux`` = pre-activation; for ReLU the activation itself works)
+* ``"glu"``:   gated forward on a 16-row-interleaved [W1|W3] weight; ``C = act(g)·u`` (N/2 columns),
+  ``aux_out`` = interleaved pre-activations
+* ``"dglu"``:  gated backward; ``acc`` = ``da`` (N columns), ``aux`` = interleaved [g|u], ``C`` = interleaved
+  [dg|du] (2N columns)
+
+CUDA (HIP) tensors run the hand-written gfx950 kernels of ``csrc/gemm.hip``; CPU tensors run the torch
+reference below (used by the CPU/gloo tests and as the numerics oracle).  There is no silent fallback:
+a GPU tensor with the native library missing raises.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import _native
+from .activations import act_code, act_fwd, act_grad
+
+LAYOUTS = {"nt": 0, "nn": 1, "tn": 2}
+EPIS = {"store": 0, "act": 1, "dact": 2, "glu": 3, "dglu": 4}
+FORCE = {None: -1, "mfma_bf16": 0, "mfma_f32": 1, "generic": 2}
+
+
+def gemm_shape(a: torch.Tensor, b: torch.Tensor, layout: str) -> tuple[int, int, int]:
+    if layout == "nt":
+        (M, K), (N, K2) = a.shape, b.shape
+    elif layout == "nn":
+        (M, K), (K2, N) = a.shape, b.shape
+    elif layout == "tn":
+        (K, M), (K2, N) = a.shape, b.shape
+    else:
+        raise ValueError(layout)
+    if K != K2:
+        raise ValueError(f"gemm {layout}: inner dims differ {tuple(a.shape)} vs {tuple(b.shape)}")
+    return M, N, K
+
+
+def out_cols(N: int, epi: str) -> int:
+    if epi == "glu":
+        return N // 2
+    if epi == "dglu":
+        return N * 2
+    return N
+
+
+def _check_rowmajor(t: torch.Tensor, name: str) -> None:
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError(f"{name} must be a row-major 2-D view (stride(1)==1), got strides {t.stride()}")
+
+
+def _glu_split(h: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """Split 16-column-interleaved [g|u] blocks into (g, u)."""
+    M, N = h.shape
+    v = h.reshape(M, N // 32, 2, 16)
+    return v[:, :, 0, :].reshape(M, N // 2), v[:, :, 1, :].reshape(M, N // 2)
+
+
+def _glu_merge(g: torch.Tensor, u: torch.Tensor) -> torch.Tensor:
+    M, F = g.shape
+    return torch.stack([g.reshape(M, F // 16, 16), u.reshape(M, F // 16, 16)], dim=2).reshape(M, 2 * F)
+
+
+def _torch_gemm(a, b, layout, out, epi, act, aux, aux_out, alpha, beta):
+    af, bf = a.float(), b.float()
+    if layout == "nt":
+        acc = af @ bf.t()
+    elif layout == "nn":
+        acc = af @ bf
+    else:
+        acc = af.t() @ bf
+    if epi == "store":
+        r = alpha * acc
+        if beta != 0.0:
+            r = r + beta * out.float()
+        out.copy_(r)
+    elif epi == "act":
+        if aux_out is not None:
+            aux_out.copy_(acc)
+        out.copy_(act_fwd(act, acc))
+    elif epi == "dact":
+        out.copy_(acc * act_grad(act, aux.float()))
+    elif epi == "glu":
+        if aux_out is not None:
+            aux_out.copy_(acc)
+        g, u = _glu_split(acc)
+        out.copy_(act_fwd(act, g) * u)
+    elif epi == "dglu":
+        g, u = _glu_split(aux.float())
+        du = acc * act_fwd(act, g)
+        dg = acc * u * act_grad(act, g)
+        out.copy_(_glu_merge(dg, du))
+    return out
+
+
+def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None = None, *, epi: str = "store",
+         act: str = "none", aux: torch.Tensor | None = None, aux_out: torch.Tensor | None = None,
+         alpha: float = 1.0, beta: float = 0.0, out_dtype: torch.dtype | None = None, group_m: int = 4,
+         force: str | None = None) -> torch.Tensor:
+    M, N, K = gemm_shape(a, b, layout)
+    if a.dtype != b.dtype:
+        raise TypeError(f"gemm operands differ in dtype: {a.dtype} vs {b.dtype}")
+    nout = out_cols(N, epi)
+    if out is None:
+        out = torch.empty((M, nout), dtype=out_dtype or a.dtype, device=a.device)
+    if out.shape != (M, nout):
+        raise ValueError(f"out has shape {tuple(out.shape)}, expected {(M, nout)}")
+    if epi in ("dact", "dglu") and aux is None:
+        raise ValueError(f"epilogue {epi} needs aux (pre-activation)")
+    if epi == "glu" and N % 32:
+        raise ValueError("gated GEMM needs N % 32 == 0 (16-row interleave)")
+    if a.device.type != "cuda":
+        return _torch_gemm(a, b, layout, out, epi, act, aux, aux_out, alpha, beta)
+
+    for t, nm in ((a, "a"), (b, "b"), (out, "out")):
+        _check_rowmajor(t, nm)
+    auxt = aux if aux is not None else aux_out
+    if auxt is not None:
+        _check_rowmajor(auxt, "aux")
+        if auxt.dtype != out.dtype:
+            raise TypeError("aux / aux_out must have the output dtype")
+    L = _native.lib()
+    in_dt, out_dt = _native.dtype_code(a.dtype), _native.dtype_code(out.dtype)
+    rc = L.dllm_gemm(in_dt, out_dt, LAYOUTS[layout], EPIS[epi], act_code(act),
+                     a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), out.data_ptr(), out.stride(0),
+                     aux.data_ptr() if aux is not None else None,
+                     aux_out.data_ptr() if aux_out is not None else None,
+                     auxt.stride(0) if auxt is not None else 0,
+                     M, N, K, float(alpha), float(beta), int(group_m), FORCE[force],
+                     _native.stream_ptr(a.device))
+    _native.check(rc, f"dllm_gemm({layout},{epi},M={M},N={N},K={K})")
+    return out
+
+
+def gemm_path(a_dtype: torch.dtype, out_dtype: torch.dtype, M: int, N: int, K: int,
+              lda: int, ldb: int, ldc: int) -> str:
+    """Which native kernel family a call would use: 'mfma_bf16', 'mfma_f32' or 'generic'."""
+    p = _native.lib().dllm_gemm_path(_native.dtype_code(a_dtype), _native.dtype_code(out_dtype), M, N, K,
+                                     lda, ldb, ldc)
+    return {0: "mfma_bf16", 1: "mfma_f32", 2: "generic"}[p]

@@ -1,0 +1,87 @@
+"""Collective wrappers: flat, zero-copy, async, one stream per role.
+
+Every call site of the reference maps to one function here:
+
+* X1 ``dist.all_reduce(grad, async_op=True)`` per tensor (train_ffns.py:165)  -> ``all_reduce`` on bucket views
+* X2 ``dist.all_gather(list, shard, async_op=True)`` + ``torch.cat`` (:203,:209) -> ``all_gather_into``
+  writing straight into the full-weight buffer (row shards concatenate contiguously, no cat, no zeros_like)
+* X3 sync ``dist.reduce_scatter(shard, list(chunk(g)))`` (:255-256)            -> async ``reduce_scatter_into``
+  from the flat full-grad buffer on its own communicator/stream (fixes the TODO at :14/:252)
+* X4/X5 sync ``dist.all_reduce(y / dx)`` (:303,:309)                           -> ``all_reduce`` on the tp role,
+  async where a consumer can wait later.
+
+With the ``nccl`` backend (RCCL over xGMI) the returned handle's ``wait()`` only makes the *current HIP
+stream* wait on the collective's stream (no host block), so compute keeps flowing.  ``world == 1`` is a
+no-op returning an already-completed handle.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+class Done:
+    """Completed-work placeholder (single-rank groups, or nothing to do)."""
+
+    def wait(self):
+        return True
+
+    def is_completed(self):
+        return True
+
+
+def _size(group) -> int:
+    if group is None or not dist.is_initialized():
+        return 1
+    return dist.get_world_size(group)
+
+
+def all_reduce(t: torch.Tensor, group, async_op: bool = True):
+    if _size(group) == 1:
+        return Done()
+    w = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
+    return w if async_op else Done()
+
+
+def all_gather_into(out: torch.Tensor, shard: torch.Tensor, group, async_op: bool = True):
+    n = _size(group)
+    if n == 1:
+        if out.data_ptr() != shard.data_ptr():
+            out.copy_(shard.view_as(out))
+        return Done()
+    if out.numel() != shard.numel() * n:
+        raise ValueError(f"all_gather_into: out {out.numel()} != {n} x shard {shard.numel()}")
+    w = dist.all_gather_into_tensor(out.view(-1), shard.reshape(-1), group=group, async_op=async_op)
+    return w if async_op else Done()
+
+
+def reduce_scatter_into(out: torch.Tensor, full: torch.Tensor, group, async_op: bool = True):
+    n = _size(group)
+    if n == 1:
+        if out.data_ptr() != full.data_ptr():
+            out.copy_(full.view_as(out))
+        return Done()
+    if full.numel() != out.numel() * n:
+        raise ValueError(f"reduce_scatter_into: full {full.numel()} != {n} x out {out.numel()}")
+    w = dist.reduce_scatter_tensor(out.view(-1), full.reshape(-1), op=dist.ReduceOp.SUM, group=group,
+                                   async_op=async_op)
+    return w if async_op else Done()
+
+
+def gather_to_rank0(t: torch.Tensor, group=None) -> list[torch.Tensor] | None:
+    """Gather equally-shaped tensors from every rank of ``group`` onto rank 0 of that group (CPU copies)."""
+    n = _size(group)
+    if n == 1:
+        return [t.detach().cpu()]
+    outs = [torch.empty_like(t) for _ in range(n)]
+    dist.all_gather(outs, t.contiguous(), group=group)
+    return [o.cpu() for o in outs]
+
+
+def barrier(group=None, device: torch.device | None = None) -> None:
+    if not dist.is_initialized():
+        return
+    if device is not None and device.type == "cuda":
+        dist.barrier(group=group, device_ids=[device.index])
+    else:
+        dist.barrier(group=group)

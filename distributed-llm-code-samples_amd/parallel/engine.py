@@ -1,0 +1,449 @@
+"""Unified FFN training engine: single device, DDP, FSDP (ZeRO-3), TP (Megatron MP) and 2-D hybrids.
+
+The reference has four separate workers (train_ffns.py:101-116 single, :156-193 DDP, :197-287 FSDP,
+:290-338 TP).  Here one engine covers all of them as points of a ``dp × tp`` mesh:
+
+    method        dp_mode  dp  tp
+    1 gpu         none     1   1
+    2 DDP         ddp      n   1
+    3 FSDP        fsdp     n   1
+    4 TP / "MP"   none     1   n
+    5 hybrid      ddp|fsdp d   t      (FSDP×TP for the Llama-3-8B-dims config)
+
+MI355X-first memory design (288 GB HBM per GPU):
+
+* **Flat buffers in completion order.**  Every rank owns one flat fp32 master buffer (plus its bf16
+  compute copy, its gradient buffer and optional Adam moments) holding, for ``l = L-1 … 0``, the
+  layer's ``W2`` then ``W1`` (= the order the backward finishes them).  Any contiguous range is
+  therefore a valid gradient bucket that becomes ready all at once — DDP buckets are plain views,
+  collectives are zero-copy, and the optimizer runs over ranges with one fused kernel.
+* **DDP**: wgrad GEMMs write straight into the flat gradient buffer; each bucket's all-reduce is issued
+  on the ``dp_ar`` communicator the moment its last gradient is written, overlapping the rest of the
+  backward (reference: per-tensor all-reduce, :164-165).  After the backward each bucket is waited
+  for (a stream wait, not a host block) and updated in place by the fused optimizer, so early buckets'
+  updates overlap late buckets' communication.
+* **FSDP**: each rank keeps a row-shard (dim 0, as :265-266) of every weight.  Forward gathers layer
+  l+1 while computing l; backward reuses the last layer's gathered weights and gathers l-1 while
+  computing l (:236-250) — into a preallocated 2-slot ring with ``all_gather_into_tensor`` (no
+  ``zeros_like``, no ``cat``).  Gradients go into a 2-slot full-layer ring and are reduce-scattered
+  **asynchronously on their own communicator** (``dp_rs``), overlapping the next layer's backward —
+  the overlap the reference could not get from one process group (:14, :252).  A shard's optimizer
+  step runs as soon as its reduce-scatter is waited for.
+* **TP**: W1 column-parallel (dim-0 rows), W2 row-parallel (dim-1 columns) (:316-319); per layer one
+  all-reduce of ``y`` in forward (:303) and one of ``dx`` in backward (:309), the latter overlapped
+  with the dW1 GEMM; the layer-0 input-grad all-reduce of the reference is skipped (its result is
+  never used).  Optional sequence parallelism keeps activations T-sharded (reduce-scatter /
+  all-gather instead of all-reduce).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from ..models.ffn import (deinterleave_w13, interleave_w13, layer_bwd, layer_fwd, needs_preact,
+                          recompute_fwd1)
+from ..ops.elementwise import adam_step_, cast_, sgd_step_
+from ..utils.config import TrainConfig
+from . import comm
+from .mesh import Mesh
+
+ALIGN = 64  # elements; keeps every view 128/256-B aligned for the LDS-DMA GEMM operand loads
+
+
+def _round_up(n: int, a: int) -> int:
+    return (n + a - 1) // a * a
+
+
+@dataclass
+class Entry:
+    layer: int
+    name: str            # "w1" (W1 or interleaved W13) | "w2"
+    shape: tuple         # owned shape (shard shape under FSDP)
+    full_shape: tuple    # local (TP-level) shape
+    offset: int = 0
+
+    @property
+    def numel(self) -> int:
+        return self.shape[0] * self.shape[1]
+
+
+class _Hooks:
+    def __init__(self, eng: "FFNTrainer", layer: int):
+        self.eng, self.layer = eng, layer
+        self.tp_work = None
+
+    def after_w2(self):
+        self.eng._grad_ready(self.layer, "w2")
+
+    def after_dx(self, dx):
+        e = self.eng
+        if e.mesh.tp > 1:
+            self.tp_work = comm.all_reduce(dx, e.mesh.group("tp"), async_op=True)
+            if not e.cfg.tp_overlap:
+                self.tp_work.wait()
+                self.tp_work = None
+
+    def after_w1(self):
+        self.eng._grad_ready(self.layer, "w1")
+        if self.tp_work is not None:
+            self.tp_work.wait()
+            self.tp_work = None
+
+
+class FFNTrainer:
+    def __init__(self, cfg: TrainConfig, mesh: Mesh, device: torch.device):
+        self.cfg, self.mesh, self.device = cfg, mesh, torch.device(device)
+        m = cfg.model
+        D, F, L = m.D, m.F, m.layers
+        t, d = mesh.tp, mesh.dp
+        if F % t:
+            raise ValueError(f"FFN dim {F} not divisible by tp={t} (train_ffns.py:317 needs equal chunks)")
+        self.D, self.F, self.L = D, F, L
+        self.F_loc = F // t
+        self.gated = m.gated
+        self.act = m.act
+        if self.gated and self.F_loc % 16:
+            raise ValueError("gated FFN needs (F / tp) % 16 == 0")
+        self.R1 = (2 if self.gated else 1) * self.F_loc
+        self.fsdp = cfg.dp_mode == "fsdp" and d > 1
+        self.ddp = cfg.dp_mode in ("ddp", "fsdp") and d > 1 and not self.fsdp
+        if d > 1 and cfg.dp_mode == "none":
+            raise ValueError("dp > 1 needs dp_mode ddp or fsdp")
+        if self.fsdp and (self.R1 % d or D % d):
+            raise ValueError(f"FSDP needs W1 rows ({self.R1}) and D ({D}) divisible by dp={d} (train_ffns.py:266)")
+        self.cd, self.gd = cfg.torch_dtype, cfg.torch_grad_dtype
+        self.sp = cfg.sequence_parallel and t > 1
+        T = cfg.tokens
+        if self.sp and T % t:
+            raise ValueError("sequence parallelism needs tokens % tp == 0")
+        self.T = T
+        self.step_count = 0
+        dev = self.device
+
+        # ---- flat owned parameter layout (completion order) ------------------------------------
+        full = {"w2": (D, self.F_loc), "w1": (self.R1, D)}
+        self.entries: list[Entry] = []
+        off = 0
+        for l in reversed(range(L)):
+            for name in ("w2", "w1"):
+                fs = full[name]
+                own = (fs[0] // d, fs[1]) if self.fsdp else fs
+                e = Entry(l, name, own, fs, off)
+                off += _round_up(e.numel, ALIGN)
+                self.entries.append(e)
+        self.total = off
+        self.entry = {(e.layer, e.name): e for e in self.entries}
+        self.master = torch.zeros(self.total, dtype=torch.float32, device=dev)
+        self.shared_copy = self.cd == torch.float32
+        self.copy = self.master if self.shared_copy else torch.zeros(self.total, dtype=self.cd, device=dev)
+        self.grads = torch.zeros(self.total, dtype=self.gd, device=dev)
+        if cfg.optimizer == "adam":
+            self.adam_m = torch.zeros(self.total, dtype=torch.float32, device=dev)
+            self.adam_v = torch.zeros(self.total, dtype=torch.float32, device=dev)
+
+        # ---- FSDP rings --------------------------------------------------------------------------
+        if self.fsdp:
+            self.wring = [{n: torch.empty(full[n], dtype=self.cd, device=dev) for n in ("w2", "w1")}
+                          for _ in range(2)]
+            self.gring = [{n: torch.empty(full[n], dtype=self.gd, device=dev) for n in ("w2", "w1")}
+                          for _ in range(2)]
+            self.ag_work = [None, None]
+            self.ag_layer = [-1, -1]
+            self.rs_pending = [None, None]  # (layer, [works])
+
+        # ---- activations -------------------------------------------------------------------------
+        Tl = T // t if self.sp else T  # tokens held per rank between layers
+        self.Tl = Tl
+        self.xs = [None] + [torch.empty((Tl, D), dtype=self.cd, device=dev) for _ in range(L)]
+        keep = cfg.recompute == "none"
+        nA = L if keep else 1
+        self.acts_a = [torch.empty((T, self.F_loc), dtype=self.cd, device=dev) for _ in range(nA)]
+        self.need_h = needs_preact(self.act, self.gated)
+        self.acts_h = ([torch.empty((T, self.R1), dtype=self.cd, device=dev) for _ in range(nA)]
+                       if self.need_h else None)
+        self.da = torch.empty((T, self.R1), dtype=self.cd, device=dev)
+        self.dxb = [torch.empty((T, D), dtype=self.cd, device=dev) for _ in range(2)]
+        if self.sp:
+            self.xfull = torch.empty((T, D), dtype=self.cd, device=dev)       # gathered layer input
+            self.yfull = torch.empty((T, D), dtype=self.cd, device=dev)       # partial output
+            self.xs_full = [torch.empty((T, D), dtype=self.cd, device=dev) for _ in range(L)] if keep else None
+            self.dyfull = torch.empty((T, D), dtype=self.cd, device=dev)
+            self.dxs = [torch.empty((Tl, D), dtype=self.cd, device=dev) for _ in range(2)]
+
+        # ---- DDP buckets -------------------------------------------------------------------------
+        self.buckets = []  # (start, end, last_entry_index)
+        if self.ddp:
+            cap = int(cfg.bucket_mb * 2**20 / self.grads.element_size()) if cfg.bucket_mb > 0 else 0
+            start = 0
+            for i, e in enumerate(self.entries):
+                end = e.offset + _round_up(e.numel, ALIGN)
+                if cap == 0 or end - start >= cap or i == len(self.entries) - 1:
+                    self.buckets.append((start, end, i))
+                    start = end
+            self.bucket_work = [None] * len(self.buckets)
+        self._entry_index = {(e.layer, e.name): i for i, e in enumerate(self.entries)}
+        self._next_bucket = 0
+
+    # ------------------------------------------------------------------------------------------------
+    # views
+    # ------------------------------------------------------------------------------------------------
+    def _view(self, flat: torch.Tensor, e: Entry) -> torch.Tensor:
+        return flat[e.offset:e.offset + e.numel].view(e.shape)
+
+    def master_view(self, l: int, name: str) -> torch.Tensor:
+        return self._view(self.master, self.entry[(l, name)])
+
+    def copy_view(self, l: int, name: str) -> torch.Tensor:
+        return self._view(self.copy, self.entry[(l, name)])
+
+    def grad_view(self, l: int, name: str) -> torch.Tensor:
+        return self._view(self.grads, self.entry[(l, name)])
+
+    def _layer_range(self, l: int) -> tuple[int, int]:
+        e2, e1 = self.entry[(l, "w2")], self.entry[(l, "w1")]
+        return e2.offset, e1.offset + _round_up(e1.numel, ALIGN)
+
+    # ------------------------------------------------------------------------------------------------
+    # parameters in / out (logical layout: per layer w1 [F,D], w2 [D,F] (+ w3 [F,D] if gated))
+    # ------------------------------------------------------------------------------------------------
+    def _local_from_full(self, p: dict) -> dict:
+        t, r = self.mesh.tp, self.mesh.tp_rank
+        Fl = self.F_loc
+        w1 = p["w1"][r * Fl:(r + 1) * Fl]
+        if self.gated:
+            w1 = interleave_w13(w1, p["w3"][r * Fl:(r + 1) * Fl])
+        w2 = p["w2"][:, r * Fl:(r + 1) * Fl]
+        return {"w1": w1, "w2": w2}
+
+    def flat_buffers(self) -> dict:
+        """Named flat fp32 state buffers sharing the parameter layout (checkpointed)."""
+        out = {"params": self.master}
+        if self.cfg.optimizer == "adam":
+            out["adam_m"], out["adam_v"] = self.adam_m, self.adam_v
+        return out
+
+    @torch.no_grad()
+    def load_full_params(self, layers: list[dict], flat: torch.Tensor | None = None) -> None:
+        """Set parameters (or another flat state buffer) from full logical tensors (identical on every
+        rank; CPU or device)."""
+        if len(layers) != self.L:
+            raise ValueError("layer count mismatch")
+        target = self.master if flat is None else flat
+        d, dr = self.mesh.dp, self.mesh.dp_rank
+        for l, p in enumerate(layers):
+            loc = self._local_from_full(p)
+            for name in ("w2", "w1"):
+                src = loc[name]
+                if self.fsdp:
+                    rows = src.shape[0] // d
+                    src = src[dr * rows:(dr + 1) * rows]
+                self._view(target, self.entry[(l, name)]).copy_(src.to(torch.float32))
+        if target is self.master and not self.shared_copy:
+            cast_(self.master, self.copy)
+
+    @torch.no_grad()
+    def local_params(self, flat: torch.Tensor | None = None) -> list[dict]:
+        """This TP rank's full local (unsharded over dp) fp32 tensors of a flat buffer, w1 de-interleaved.
+        Collective over the dp group under FSDP."""
+        src = self.master if flat is None else flat
+        out = []
+        for l in range(self.L):
+            p = {}
+            for name in ("w1", "w2"):
+                mv = self._view(src, self.entry[(l, name)])
+                if self.fsdp:
+                    full = torch.empty(self.entry[(l, name)].full_shape, dtype=torch.float32, device=self.device)
+                    comm.all_gather_into(full, mv.contiguous(), self.mesh.group("dp_ag"), async_op=False)
+                    mv = full
+                p[name] = mv
+            if self.gated:
+                w1, w3 = deinterleave_w13(p["w1"])
+                p["w1"], p["w3"] = w1, w3
+            out.append(p)
+        return out
+
+    @torch.no_grad()
+    def gather_full_params(self, flat: torch.Tensor | None = None) -> list[dict] | None:
+        """Full logical fp32 tensors on CPU at global rank 0 (None elsewhere).  Collective."""
+        loc = self.local_params(flat)
+        res = []
+        for p in loc:
+            q = {}
+            for name, t in p.items():
+                parts = comm.gather_to_rank0(t.contiguous(), self.mesh.group("tp"))
+                q[name] = torch.cat(parts, dim=1 if name == "w2" else 0)
+            res.append(q)
+        return res if self.mesh.rank == 0 else None
+
+    # ------------------------------------------------------------------------------------------------
+    # optimizer over a flat range
+    # ------------------------------------------------------------------------------------------------
+    def _opt(self, s: int, e: int) -> None:
+        cfg = self.cfg
+        master, grad = self.master[s:e], self.grads[s:e]
+        copy = None if self.shared_copy else self.copy[s:e]
+        if cfg.optimizer == "sgd":
+            sgd_step_(master, grad, cfg.lr, copy=copy)
+        else:
+            adam_step_(master, grad, self.adam_m[s:e], self.adam_v[s:e], self.step_count, cfg.lr,
+                       cfg.adam_b1, cfg.adam_b2, cfg.adam_eps, cfg.weight_decay, copy=copy)
+
+    # ------------------------------------------------------------------------------------------------
+    # communication hooks
+    # ------------------------------------------------------------------------------------------------
+    def _grad_ready(self, l: int, name: str) -> None:
+        if self.ddp:
+            idx = self._entry_index[(l, name)]
+            while self._next_bucket < len(self.buckets) and self.buckets[self._next_bucket][2] <= idx:
+                b = self._next_bucket
+                s, e, _ = self.buckets[b]
+                self.bucket_work[b] = comm.all_reduce(self.grads[s:e], self.mesh.group("dp_ar"), async_op=True)
+                self._next_bucket += 1
+        elif self.fsdp and name == "w1":
+            slot = l % 2
+            g = self.gring[slot]
+            works = [comm.reduce_scatter_into(self.grad_view(l, n), g[n], self.mesh.group("dp_rs"), async_op=True)
+                     for n in ("w2", "w1")]
+            self.rs_pending[slot] = (l, works)
+
+    def _fsdp_finish_rs(self, slot: int) -> None:
+        pend = self.rs_pending[slot]
+        if pend is None:
+            return
+        l, works = pend
+        for w in works:
+            w.wait()
+        s, e = self._layer_range(l)
+        self._opt(s, e)
+        self.rs_pending[slot] = None
+
+    def _fsdp_gather(self, l: int) -> None:
+        slot = l % 2
+        grp = self.mesh.group("dp_ag")
+        self.ag_work[slot] = [comm.all_gather_into(self.wring[slot][n], self.copy_view(l, n), grp, async_op=True)
+                              for n in ("w2", "w1")]
+        self.ag_layer[slot] = l
+
+    def _fsdp_weights(self, l: int) -> tuple[torch.Tensor, torch.Tensor]:
+        slot = l % 2
+        if self.ag_layer[slot] != l:
+            raise RuntimeError(f"FSDP ring slot {slot} holds layer {self.ag_layer[slot]}, wanted {l}")
+        if self.ag_work[slot] is not None:
+            for w in self.ag_work[slot]:
+                w.wait()
+            self.ag_work[slot] = None
+        return self.wring[slot]["w1"], self.wring[slot]["w2"]
+
+    # ------------------------------------------------------------------------------------------------
+    # one training step
+    # ------------------------------------------------------------------------------------------------
+    def train_step(self, x: torch.Tensor, dy: torch.Tensor) -> torch.Tensor:
+        """Forward + backward + gradient communication + optimizer for one batch.
+
+        ``x``/``dy`` are ``[T, D]`` in the compute dtype (under sequence parallelism, the full T: each
+        rank keeps its T/tp slice).  Returns the forward output ``y`` (this rank's view).
+        """
+        cfg = self.cfg
+        L, act, gated = self.L, self.act, self.gated
+        self.step_count += 1
+        keep = cfg.recompute == "none"
+        tpg = self.mesh.group("tp")
+        if self.sp:
+            t, r = self.mesh.tp, self.mesh.tp_rank
+            x = x[r * self.Tl:(r + 1) * self.Tl]
+            dy = dy[r * self.Tl:(r + 1) * self.Tl]
+        self.xs[0] = x
+
+        # ---------------- forward ----------------
+        if self.fsdp:
+            self._fsdp_gather(0)
+        for l in range(L):
+            if self.fsdp:
+                w1, w2 = self._fsdp_weights(l)
+                if l + 1 < L:
+                    self._fsdp_gather(l + 1)
+            else:
+                w1, w2 = self.copy_view(l, "w1"), self.copy_view(l, "w2")
+            a = self.acts_a[l if keep else 0]
+            h = (self.acts_h[l if keep else 0]) if self.need_h else None
+            if self.sp:
+                xin = self.xs_full[l] if keep else self.xfull
+                comm.all_gather_into(xin, self.xs[l], tpg, async_op=True).wait()
+                layer_fwd(xin, w1, w2, act, gated, a, h, self.yfull)
+                comm.reduce_scatter_into(self.xs[l + 1], self.yfull, tpg, async_op=True).wait()
+            else:
+                layer_fwd(self.xs[l], w1, w2, act, gated, a, h, self.xs[l + 1])
+                if self.mesh.tp > 1:
+                    comm.all_reduce(self.xs[l + 1], tpg, async_op=True).wait()
+        y = self.xs[L]
+
+        # ---------------- backward ----------------
+        self._next_bucket = 0
+        if self.fsdp and L >= 2 and self.ag_layer[(L - 2) % 2] != L - 2:
+            # the forward left layers L-1 and L-2 in the ring; weights do not change until the
+            # optimizer runs, so the reference's re-gather of L-2 (:245) is skipped when still resident
+            self._fsdp_gather(L - 2)
+        g = dy
+        for l in reversed(range(L)):
+            if self.fsdp:
+                if l < L - 1:
+                    w1, w2 = self._fsdp_weights(l)
+                    if l >= 1:
+                        self._fsdp_gather(l - 1)
+                else:
+                    w1, w2 = self._fsdp_weights(l)
+                slot = l % 2
+                self._fsdp_finish_rs(slot)  # slot's previous grads (layer l+2) must be reduced first
+                gw1, gw2 = self.gring[slot]["w1"], self.gring[slot]["w2"]
+            else:
+                w1, w2 = self.copy_view(l, "w1"), self.copy_view(l, "w2")
+                gw1, gw2 = self.grad_view(l, "w1"), self.grad_view(l, "w2")
+            if keep:
+                a = self.acts_a[l]
+                h = self.acts_h[l] if self.need_h else None
+            else:
+                a = self.acts_a[0]
+                h = self.acts_h[0] if self.need_h else None
+            need_dx = l > 0 or not cfg.skip_input_grad
+            hooks = _Hooks(self, l)
+            if self.sp:
+                # gather dy (T-sharded) and the layer input; dx partial -> reduce-scatter
+                comm.all_gather_into(self.dyfull, g, tpg, async_op=True).wait()
+                xin = self.xs_full[l] if keep else self.xfull
+                if not keep:
+                    comm.all_gather_into(xin, self.xs[l], tpg, async_op=True).wait()
+                    recompute_fwd1(xin, w1, act, gated, a, h)
+                hooks_sp = _SPHooks(self, l)
+                dxp = layer_bwd(self.dyfull, xin, w1, w2, act, gated, a, h, gw1, gw2, self.da,
+                                self.dxb[l % 2] if need_dx else None, hooks_sp)
+                if dxp is not None:
+                    out = self.dxs[l % 2]
+                    comm.reduce_scatter_into(out, dxp, tpg, async_op=True).wait()
+                    g = out
+            else:
+                if not keep:
+                    recompute_fwd1(self.xs[l], w1, act, gated, a, h)
+                dx = layer_bwd(g, self.xs[l], w1, w2, act, gated, a, h, gw1, gw2, self.da,
+                               self.dxb[l % 2] if need_dx else None, hooks)
+                if dx is not None:
+                    g = dx
+
+        # ---------------- optimizer ----------------
+        if self.ddp:
+            for b, (s, e, _) in enumerate(self.buckets):
+                self.bucket_work[b].wait()
+                self._opt(s, e)
+        elif self.fsdp:
+            for slot in ((L - 1) % 2, L % 2):
+                self._fsdp_finish_rs(slot)
+        else:
+            self._opt(0, self.total)
+        return y
+
+
+class _SPHooks(_Hooks):
+    """Sequence-parallel variant: the dx reduce-scatter is issued by the caller after the layer."""
+
+    def after_dx(self, dx):
+        return None

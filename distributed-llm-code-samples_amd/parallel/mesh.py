@@ -1,0 +1,123 @@
+"""Process bootstrap and the 2-D (data × tensor) device mesh.
+
+Reference: ``init_process`` sets ``MASTER_ADDR=127.0.0.1``/``MASTER_PORT=29500`` and calls
+``dist.init_process_group("nccl", rank, world_size=nGPUs)`` (train_ffns.py:121-127); every method uses
+all GPUs on one axis and one process group, so FSDP's reduce-scatter serialises behind its prefetch
+all-gather on the single NCCL stream (the author's TODO, train_ffns.py:14,252).
+
+Here: one process per GPU (torchrun env or our own spawner), backend ``nccl`` (= RCCL over xGMI on ROCm)
+or ``gloo`` (CPU plumbing), and a ``Mesh`` of ``dp × tp`` ranks (tp fastest-varying, so a TP group is a
+block of neighbouring GPUs).  Each communication *role* gets its own process group — and therefore its
+own RCCL communicator and HIP stream — so DDP gradient all-reduce, FSDP parameter all-gather, FSDP
+gradient reduce-scatter and TP activation all-reduce can run concurrently with each other and with
+compute:
+
+    role      ranks        used by
+    dp_ar     dp group     DDP bucketed gradient all-reduce
+    dp_ag     dp group     FSDP parameter all-gather (prefetch)
+    dp_rs     dp group     FSDP gradient reduce-scatter
+    tp        tp group     Megatron activation / input-grad all-reduce (or SP reduce-scatter/all-gather)
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass, field
+
+import torch
+import torch.distributed as dist
+
+ROLES = ("dp_ar", "dp_ag", "dp_rs", "tp")
+
+
+def init_distributed(backend: str, rank: int | None = None, world_size: int | None = None,
+                     master_addr: str | None = None, master_port: int | None = None,
+                     timeout_s: float = 600.0) -> tuple[int, int]:
+    """Initialise the default process group from explicit args or the torchrun environment."""
+    if dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    rank = int(os.environ.get("RANK", 0)) if rank is None else rank
+    world_size = int(os.environ.get("WORLD_SIZE", 1)) if world_size is None else world_size
+    os.environ["MASTER_ADDR"] = master_addr or os.environ.get("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(master_port or os.environ.get("MASTER_PORT", "29500"))
+    kw = {}
+    if backend == "nccl":
+        local = int(os.environ.get("LOCAL_RANK", rank))
+        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+        kw["device_id"] = torch.device("cuda", torch.cuda.current_device())
+    dist.init_process_group(backend, rank=rank, world_size=world_size,
+                            timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    return rank, world_size
+
+
+@dataclass
+class Mesh:
+    """``world = dp × tp`` ranks; ``rank = dp_rank * tp + tp_rank``."""
+
+    dp: int = 1
+    tp: int = 1
+    rank: int = 0
+    groups: dict = field(default_factory=dict)
+    dp_ranks: list = field(default_factory=list)
+    tp_ranks: list = field(default_factory=list)
+
+    @property
+    def world(self) -> int:
+        return self.dp * self.tp
+
+    @property
+    def dp_rank(self) -> int:
+        return self.rank // self.tp
+
+    @property
+    def tp_rank(self) -> int:
+        return self.rank % self.tp
+
+    def group(self, role: str):
+        return self.groups.get(role)
+
+    @classmethod
+    def build(cls, dp: int, tp: int, separate_streams: bool = True) -> "Mesh":
+        """Create the role process groups (collective: every rank must call it with the same args)."""
+        world = dist.get_world_size() if dist.is_initialized() else 1
+        rank = dist.get_rank() if dist.is_initialized() else 0
+        if dp * tp != world:
+            raise ValueError(f"mesh dp={dp} x tp={tp} != world size {world}")
+        m = cls(dp=dp, tp=tp, rank=rank)
+        m.dp_ranks = [d * tp + m.tp_rank for d in range(dp)]
+        m.tp_ranks = [m.dp_rank * tp + t for t in range(tp)]
+        if world == 1 or not dist.is_initialized():
+            return m
+        # every rank creates every group in the same order (new_group is collective)
+        for role in ROLES:
+            if role.startswith("dp"):
+                if dp == 1:
+                    continue
+                if not separate_streams and role != "dp_ar" and "dp_ar" in m.groups:
+                    m.groups[role] = m.groups["dp_ar"]
+                    continue
+                if dp == world:
+                    grp = dist.new_group(list(range(world)))
+                    m.groups[role] = grp
+                else:
+                    mine = None
+                    for t in range(tp):
+                        ranks = [d * tp + t for d in range(dp)]
+                        g = dist.new_group(ranks)
+                        if rank in ranks:
+                            mine = g
+                    m.groups[role] = mine
+            else:
+                if tp == 1:
+                    continue
+                if tp == world:
+                    m.groups[role] = dist.new_group(list(range(world)))
+                else:
+                    mine = None
+                    for d in range(dp):
+                        ranks = [d * tp + t for t in range(tp)]
+                        g = dist.new_group(ranks)
+                        if rank in ranks:
+                            mine = g
+                    m.groups[role] = mine
+        return m

@@ -1,0 +1,116 @@
+"""Run configuration: a superset of the reference CLI (train_ffns.py:343-350).
+
+Reference flags keep their short/long names and defaults; north-star extras are added with defaults
+that reproduce the reference semantics (ReLU, FFN = 4·D, SGD, LR = 1e-5, summed DP gradients).
+"""
+from __future__ import annotations
+
+import argparse
+import dataclasses
+from dataclasses import dataclass
+
+import torch
+
+LR = 1e-5            # train_ffns.py:29
+DLOSS_DX_COEF = 0.1  # train_ffns.py:30
+INIT_SCALE = 2e-2    # train_ffns.py:35
+SEED_RANGE = 100_000  # train_ffns.py:360
+METHODS = {0: "all", 1: "1gpu", 2: "ddp", 3: "fsdp", 4: "tp", 5: "hybrid"}
+
+
+@dataclass
+class ModelConfig:
+    model_size: int = 4              # D  (-d)
+    ffn_dim: int = 0                 # F; 0 -> 4·D (train_ffns.py:361)
+    layers: int = 1                  # L  (-l)
+    act: str = "relu"                # relu | silu | gelu
+    gated: bool = False              # SwiGLU-style W1/W3 gate (Llama FFN)
+
+    @property
+    def F(self) -> int:
+        return self.ffn_dim or 4 * self.model_size
+
+    @property
+    def D(self) -> int:
+        return self.model_size
+
+    def num_params(self) -> int:
+        per = (3 if self.gated else 2) * self.D * self.F
+        return per * self.layers
+
+
+@dataclass
+class TrainConfig:
+    model: ModelConfig = dataclasses.field(default_factory=ModelConfig)
+    batch_size: int = 8              # -bs
+    seq_len: int = 1024              # -n
+    num_steps: int = 1               # -s
+    random_seed: int = 0             # -r (0 = unseeded, train_ffns.py:355-358)
+    dtype: str = "fp32"              # compute dtype: fp32 (reference parity) | bf16
+    grad_dtype: str = "fp32"         # dtype of gradients / gradient collectives
+    optimizer: str = "sgd"           # sgd (reference) | adam
+    lr: float = LR
+    adam_b1: float = 0.9
+    adam_b2: float = 0.95
+    adam_eps: float = 1e-8
+    weight_decay: float = 0.0
+    dp_mode: str = "none"            # none | ddp | fsdp
+    dp: int = 1
+    tp: int = 1
+    sequence_parallel: bool = False  # Megatron SP for the TP path (RS/AG over T instead of AR)
+    recompute: str = "none"          # none (save activations) | full (reference: recompute h in bwd)
+    bucket_mb: float = 0.0           # DDP bucket cap; 0 = one bucket per weight tensor
+    data: str = "device"             # device (Philox on GPU) | cpu_compat (reference CPU generator)
+    skip_input_grad: bool = True     # layer-0 dx is never consumed (reference computes it, :68)
+    separate_streams: bool = True    # one communicator/stream per comm role
+    tp_overlap: bool = True          # overlap the TP dx all-reduce with the dW1 GEMM
+
+    @property
+    def tokens(self) -> int:
+        return self.batch_size * self.seq_len
+
+    @property
+    def torch_dtype(self) -> torch.dtype:
+        return {"fp32": torch.float32, "bf16": torch.bfloat16}[self.dtype]
+
+    @property
+    def torch_grad_dtype(self) -> torch.dtype:
+        return {"fp32": torch.float32, "bf16": torch.bfloat16}[self.grad_dtype]
+
+
+def add_reference_args(p: argparse.ArgumentParser) -> None:
+    p.add_argument("-s", "--num_steps", type=int, default=1)
+    p.add_argument("-bs", "--batch_size", type=int, default=8)
+    p.add_argument("-n", "--seq_len", type=int, default=1024)
+    p.add_argument("-l", "--layers", type=int, default=1)
+    p.add_argument("-d", "--model_size", type=int, default=4)
+    p.add_argument("-m", "--method", type=int, default=0,
+                   help="0=all, 1=1gpu, 2=DDP, 3=FSDP, 4=TP (MP), 5=hybrid FSDP/DDP x TP")
+    p.add_argument("-r", "--random_seed", type=int, default=0)
+
+
+def add_extended_args(p: argparse.ArgumentParser) -> None:
+    p.add_argument("--dtype", choices=["fp32", "bf16"], default="fp32")
+    p.add_argument("--grad_dtype", choices=["fp32", "bf16"], default=None)
+    p.add_argument("--act", choices=["relu", "silu", "gelu"], default="relu")
+    p.add_argument("--ffn_dim", type=int, default=0)
+    p.add_argument("--gated", action="store_true")
+    p.add_argument("--optimizer", choices=["sgd", "adam"], default="sgd")
+    p.add_argument("--lr", type=float, default=LR)
+    p.add_argument("--weight_decay", type=float, default=0.0)
+    p.add_argument("--backend", choices=["auto", "nccl", "rccl", "gloo"], default="auto")
+    p.add_argument("--nprocs", type=int, default=0, help="ranks to spawn (0 = all visible GPUs)")
+    p.add_argument("--dp", type=int, default=0)
+    p.add_argument("--tp", type=int, default=0)
+    p.add_argument("--hybrid_dp_mode", choices=["ddp", "fsdp"], default="fsdp")
+    p.add_argument("--sequence_parallel", action="store_true")
+    p.add_argument("--recompute", choices=["none", "full"], default="none")
+    p.add_argument("--bucket_mb", type=float, default=0.0)
+    p.add_argument("--data", choices=["device", "cpu_compat"], default="cpu_compat")
+    p.add_argument("--ckpt_dir", default="")
+    p.add_argument("--ckpt_format", choices=["consolidated", "sharded"], default="consolidated")
+    p.add_argument("--resume", default="")
+    p.add_argument("--profile", default="", help="write a torch.profiler chrome trace (rank 0) to this path")
+    p.add_argument("--metrics_jsonl", default="")
+    p.add_argument("--strict", action="store_true", help="exit non-zero when method results disagree")
+    p.add_argument("--master_port", type=int, default=29500)

@@ -1,0 +1,220 @@
+"""Numerics of the hand-written gfx950 GEMM kernels against plain PyTorch fp32/fp64 references.
+
+Covers all three operand layouts (NT fwd, NN dgrad, TN wgrad), every fused epilogue, the three kernel
+families (bf16 256² MFMA, fp32 MFMA, generic), exact-integer layout checks (A = I with an asymmetric B,
+cdna_hip_programming.md §3), strided views, beta-accumulation and odd shapes.
+"""
+import os
+
+import pytest
+import torch
+
+from dllm.ops.gemm import gemm, gemm_path
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _mk(shape, dtype, seed, scale=1.0, integer=False):
+    g = torch.Generator().manual_seed(seed)
+    if integer:
+        t = torch.randint(-3, 4, shape, generator=g).float()
+    else:
+        t = torch.randn(shape, generator=g) * scale
+    return t.to(dtype)
+
+
+def _operands(layout, M, N, K, dtype, seed=0, integer=False):
+    if layout == "nt":
+        a, b = _mk((M, K), dtype, seed, integer=integer), _mk((N, K), dtype, seed + 1, integer=integer)
+    elif layout == "nn":
+        a, b = _mk((M, K), dtype, seed, integer=integer), _mk((K, N), dtype, seed + 1, integer=integer)
+    else:
+        a, b = _mk((K, M), dtype, seed, integer=integer), _mk((K, N), dtype, seed + 1, integer=integer)
+    return a, b
+
+
+def _ref(a, b, layout):
+    a, b = a.double(), b.double()
+    return {"nt": lambda: a @ b.t(), "nn": lambda: a @ b, "tn": lambda: a.t() @ b}[layout]()
+
+
+def test_native_library_is_loaded():
+    import dllm._native as nat
+
+    nat.lib()
+    maps = open("/proc/self/maps").read()
+    assert "_dllm_native.so" in maps
+    hip = {l.split()[-1] for l in maps.splitlines() if "libamdhip64" in l}
+    assert len(hip) == 1, f"more than one HIP runtime mapped: {hip}"
+
+
+@pytest.mark.parametrize("layout", ["nt", "nn", "tn"])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 320), (768, 512, 1024)])
+def test_bf16_mfma_exact_integers(layout, M, N, K):
+    a, b = _operands(layout, M, N, K, torch.bfloat16, seed=M + N + K, integer=True)
+    assert gemm_path(torch.bfloat16, torch.float32, M, N, K, a.stride(0), b.stride(0), N) == "mfma_bf16"
+    out = gemm(a.to(DEV), b.to(DEV), layout, out_dtype=torch.float32, force="mfma_bf16")
+    torch.cuda.synchronize()
+    assert torch.equal(out.cpu().double(), _ref(a, b, layout))
+
+
+@pytest.mark.parametrize("layout", ["nt", "nn", "tn"])
+def test_identity_asymmetric(layout):
+    n = 256
+    eye = torch.eye(n, dtype=torch.bfloat16)
+    B = (torch.arange(n * n).reshape(n, n) % 7 - 3).to(torch.bfloat16) * torch.arange(1, n + 1).reshape(n, 1).remainder(5).to(torch.bfloat16)
+    out = gemm(eye.to(DEV), B.to(DEV), layout, out_dtype=torch.float32, force="mfma_bf16").cpu()
+    want = {"nt": B.t(), "nn": B, "tn": B}[layout].float()
+    assert torch.equal(out, want)
+
+
+@pytest.mark.parametrize("layout", ["nt", "nn", "tn"])
+@pytest.mark.parametrize("out_dtype", [torch.bfloat16, torch.float32])
+def test_bf16_mfma_random(layout, out_dtype):
+    M, N, K = 512, 1024, 768
+    a, b = _operands(layout, M, N, K, torch.bfloat16, seed=5)
+    out = gemm(a.to(DEV), b.to(DEV), layout, out_dtype=out_dtype, force="mfma_bf16").cpu().double()
+    ref = _ref(a, b, layout)
+    err = (out - ref).abs().max() / ref.abs().max()
+    assert err < (8e-3 if out_dtype == torch.bfloat16 else 1e-5), err
+
+
+@pytest.mark.parametrize("act", ["relu", "silu", "gelu"])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_epilogues_match_torch(act, dtype):
+    M, N, K = 256, 512, 256
+    force = "mfma_bf16" if dtype == torch.bfloat16 else "mfma_f32"
+    x, w1 = _operands("nt", M, N, K, dtype, seed=11)
+    # fwd: act with aux_out
+    a_cpu = torch.empty(M, N, dtype=dtype)
+    h_cpu = torch.empty(M, N, dtype=dtype)
+    gemm(x, w1, "nt", out=a_cpu, epi="act", act=act, aux_out=h_cpu)
+    a_g = torch.empty(M, N, dtype=dtype, device=DEV)
+    h_g = torch.empty(M, N, dtype=dtype, device=DEV)
+    gemm(x.to(DEV), w1.to(DEV), "nt", out=a_g, epi="act", act=act, aux_out=h_g, force=force)
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
+    torch.testing.assert_close(h_g.cpu().float(), h_cpu.float(), rtol=tol, atol=tol)
+    torch.testing.assert_close(a_g.cpu().float(), a_cpu.float(), rtol=tol, atol=tol)
+    # dgrad with act' mask: da = (dy · W2) * act'(h)    (NN)
+    dy, w2 = _operands("nn", M, N, 384, dtype, seed=12)  # dy [M, 384], w2 [384, N]
+    da_cpu = torch.empty(M, N, dtype=dtype)
+    gemm(dy, w2, "nn", out=da_cpu, epi="dact", act=act, aux=h_cpu)
+    da_g = torch.empty(M, N, dtype=dtype, device=DEV)
+    gemm(dy.to(DEV), w2.to(DEV), "nn", out=da_g, epi="dact", act=act, aux=h_cpu.to(DEV), force=force)
+    torch.testing.assert_close(da_g.cpu().float(), da_cpu.float(), rtol=tol, atol=tol * 4)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_gated_epilogues(dtype):
+    M, N, K = 256, 512, 256  # N = 2F interleaved
+    force = "mfma_bf16" if dtype == torch.bfloat16 else "mfma_f32"
+    x, w13 = _operands("nt", M, N, K, dtype, seed=21)
+    a_c, h_c = torch.empty(M, N // 2, dtype=dtype), torch.empty(M, N, dtype=dtype)
+    gemm(x, w13, "nt", out=a_c, epi="glu", act="silu", aux_out=h_c)
+    a_g, h_g = torch.empty(M, N // 2, dtype=dtype, device=DEV), torch.empty(M, N, dtype=dtype, device=DEV)
+    gemm(x.to(DEV), w13.to(DEV), "nt", out=a_g, epi="glu", act="silu", aux_out=h_g, force=force)
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
+    torch.testing.assert_close(h_g.cpu().float(), h_c.float(), rtol=tol, atol=tol)
+    torch.testing.assert_close(a_g.cpu().float(), a_c.float(), rtol=tol, atol=tol)
+    dy, w2 = _operands("nn", M, N // 2, 256, dtype, seed=22)
+    d_c = torch.empty(M, N, dtype=dtype)
+    gemm(dy, w2, "nn", out=d_c, epi="dglu", act="silu", aux=h_c)
+    d_g = torch.empty(M, N, dtype=dtype, device=DEV)
+    gemm(dy.to(DEV), w2.to(DEV), "nn", out=d_g, epi="dglu", act="silu", aux=h_c.to(DEV), force=force)
+    torch.testing.assert_close(d_g.cpu().float(), d_c.float(), rtol=tol, atol=tol * 4)
+
+
+@pytest.mark.parametrize("layout", ["nt", "nn", "tn"])
+def test_fp32_mfma_exact_f32(layout):
+    M, N, K = 256, 384, 272
+    a, b = _operands(layout, M, N, K, torch.float32, seed=3)
+    assert gemm_path(torch.float32, torch.float32, M, N, K, a.stride(0), b.stride(0), N) == "mfma_f32"
+    out = gemm(a.to(DEV), b.to(DEV), layout, force="mfma_f32").cpu().double()
+    ref = _ref(a, b, layout)
+    assert ((out - ref).abs().max() / ref.abs().max()) < 1e-6
+
+
+@pytest.mark.parametrize("layout", ["nt", "nn", "tn"])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("epi", ["store", "act", "dact"])
+def test_generic_odd_shapes(layout, dtype, epi):
+    M, N, K = 100, 70, 37
+    a, b = _operands(layout, M, N, K, dtype, seed=7)
+    aux = _mk((M, N), dtype, 9) if epi == "dact" else None
+    out_c = torch.empty(M, N, dtype=dtype)
+    gemm(a, b, layout, out=out_c, epi=epi, act="gelu", aux=aux)
+    out_g = torch.empty(M, N, dtype=dtype, device=DEV)
+    gemm(a.to(DEV), b.to(DEV), layout, out=out_g, epi=epi, act="gelu",
+         aux=aux.to(DEV) if aux is not None else None, force="generic")
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+    torch.testing.assert_close(out_g.cpu().float(), out_c.float(), rtol=tol, atol=tol)
+
+
+def test_strided_views_and_beta():
+    M, N, K = 256, 512, 256
+    big_a = _mk((M, K + 64), torch.bfloat16, 1)
+    big_b = _mk((N, K + 128), torch.bfloat16, 2)
+    a, b = big_a[:, :K], big_b[:, 64:64 + K]
+    c0 = _mk((M, N), torch.float32, 3)
+    out = c0.clone().to(DEV)
+    gemm(big_a.to(DEV)[:, :K], big_b.to(DEV)[:, 64:64 + K], "nt", out=out, beta=1.0, alpha=0.5,
+         force="mfma_bf16")
+    ref = 0.5 * _ref(a, b, "nt") + c0.double()
+    assert ((out.cpu().double() - ref).abs().max() / ref.abs().max()) < 1e-5
+
+
+def test_rng_matches_cpu_philox():
+    from dllm.ops.elementwise import rng_normal_
+
+    g = torch.empty(4099, device=DEV)
+    c = torch.empty(4099)
+    rng_normal_(g, seed=123, stream_id=1, scale=0.5)
+    rng_normal_(c, seed=123, stream_id=1, scale=0.5)
+    torch.testing.assert_close(g.cpu(), c, rtol=1e-4, atol=1e-4)
+    big = torch.empty(1 << 22, device=DEV, dtype=torch.bfloat16)
+    rng_normal_(big, seed=9)
+    f = big.float()
+    assert abs(f.mean().item()) < 5e-3 and abs(f.std().item() - 1) < 5e-3
+
+
+@pytest.mark.parametrize("gdt", [torch.float32, torch.bfloat16])
+def test_optimizers_match_torch(gdt):
+    from dllm.ops.elementwise import adam_step_, sgd_step_
+
+    n = 4096 + 64
+    p = torch.randn(n)
+    gr = torch.randn(n).to(gdt)
+    pg, cg = p.clone().to(DEV), torch.empty(n, dtype=torch.bfloat16, device=DEV)
+    sgd_step_(pg, gr.to(DEV), 0.1, copy=cg)
+    pc = p.clone()
+    sgd_step_(pc, gr, 0.1)
+    torch.testing.assert_close(pg.cpu(), pc)
+    torch.testing.assert_close(cg.cpu().float(), pc.to(torch.bfloat16).float())
+    m, v = torch.zeros(n), torch.zeros(n)
+    mg, vg = m.to(DEV), v.to(DEV)
+    pa, pag = p.clone(), p.clone().to(DEV)
+    for step in (1, 2, 3):
+        adam_step_(pa, gr, m, v, step, 1e-3, wd=0.01)
+        adam_step_(pag, gr.to(DEV), mg, vg, step, 1e-3, wd=0.01)
+    torch.testing.assert_close(pag.cpu(), pa, rtol=1e-5, atol=1e-6)
+
+
+def test_streams_and_events_overlap():
+    """test_torch_cuda_stream.py done with assertions: native GEMMs on several HIP streams, joined by events."""
+    streams = [torch.cuda.Stream() for _ in range(4)]
+    a = [_mk((256, 256), torch.bfloat16, i).to(DEV) for i in range(4)]
+    b = [_mk((256, 256), torch.bfloat16, 10 + i).to(DEV) for i in range(4)]
+    outs = [torch.empty(256, 256, dtype=torch.float32, device=DEV) for _ in range(4)]
+    cur = torch.cuda.current_stream()
+    for s in streams:
+        s.wait_stream(cur)
+    for i, s in enumerate(streams):
+        with torch.cuda.stream(s):
+            for _ in range(10):
+                gemm(a[i], b[i], "nt", out=outs[i])
+    for s in streams:
+        cur.wait_stream(s)
+    total = sum(outs)
+    ref = sum(_ref(x.cpu(), y.cpu(), "nt") for x, y in zip(a, b))
+    assert ((total.cpu().double() - ref).abs().max() / ref.abs().max()) < 1e-5
