@@ -36,14 +36,8 @@ def _mulhilo(a: int, b: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
     return hi, lo
 
 
-def _philox_normal_cpu(n: int, seed: int, stream_id: int, scale: float) -> torch.Tensor:
-    n4 = (n + 3) // 4
-    idx = torch.arange(n4, dtype=torch.int64)
-    c0 = idx & 0xFFFFFFFF
-    c1 = (idx >> 32) & 0xFFFFFFFF
-    c2 = torch.full_like(idx, stream_id & 0xFFFFFFFF)
-    c3 = torch.full_like(idx, (stream_id >> 32) & 0xFFFFFFFF)
-    k0, k1 = seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF
+def philox4x32_10(c0, c1, c2, c3, k0: int, k1: int):
+    """Vectorised Philox4x32-10 on int64 tensors holding uint32 lanes (same rounds as csrc/elementwise.hip)."""
     M0, M1, W0, W1 = 0xD2511F53, 0xCD9E8D57, 0x9E3779B9, 0xBB67AE85
     for _ in range(10):
         hi0, lo0 = _mulhilo(M0, c0)
@@ -51,6 +45,16 @@ def _philox_normal_cpu(n: int, seed: int, stream_id: int, scale: float) -> torch
         c0, c1, c2, c3 = hi1 ^ c1 ^ k0, lo1, hi0 ^ c3 ^ k1, lo0
         k0 = (k0 + W0) & 0xFFFFFFFF
         k1 = (k1 + W1) & 0xFFFFFFFF
+    return c0, c1, c2, c3
+
+
+def _philox_normal_cpu(n: int, seed: int, stream_id: int, scale: float) -> torch.Tensor:
+    n4 = (n + 3) // 4
+    idx = torch.arange(n4, dtype=torch.int64)
+    c0, c1, c2, c3 = philox4x32_10(idx & 0xFFFFFFFF, (idx >> 32) & 0xFFFFFFFF,
+                                   torch.full_like(idx, stream_id & 0xFFFFFFFF),
+                                   torch.full_like(idx, (stream_id >> 32) & 0xFFFFFFFF),
+                                   seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
     inv = 2.3283064365386963e-10
 
     def bm(a, b):

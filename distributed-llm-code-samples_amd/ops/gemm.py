@@ -72,7 +72,8 @@ def _glu_merge(g: torch.Tensor, u: torch.Tensor) -> torch.Tensor:
 
 
 def _torch_gemm(a, b, layout, out, epi, act, aux, aux_out, alpha, beta):
-    af, bf = a.float(), b.float()
+    acc_dt = torch.promote_types(a.dtype, torch.float32)  # fp32 accumulation (fp64 stays fp64 for oracles)
+    af, bf = a.to(acc_dt), b.to(acc_dt)
     if layout == "nt":
         acc = af @ bf.t()
     elif layout == "nn":
@@ -82,21 +83,21 @@ def _torch_gemm(a, b, layout, out, epi, act, aux, aux_out, alpha, beta):
     if epi == "store":
         r = alpha * acc
         if beta != 0.0:
-            r = r + beta * out.float()
+            r = r + beta * out.to(acc_dt)
         out.copy_(r)
     elif epi == "act":
         if aux_out is not None:
             aux_out.copy_(acc)
         out.copy_(act_fwd(act, acc))
     elif epi == "dact":
-        out.copy_(acc * act_grad(act, aux.float()))
+        out.copy_(acc * act_grad(act, aux.to(acc_dt)))
     elif epi == "glu":
         if aux_out is not None:
             aux_out.copy_(acc)
         g, u = _glu_split(acc)
         out.copy_(act_fwd(act, g) * u)
     elif epi == "dglu":
-        g, u = _glu_split(aux.float())
+        g, u = _glu_split(aux.to(acc_dt))
         du = acc * act_fwd(act, g)
         dg = acc * u * act_grad(act, g)
         out.copy_(_glu_merge(dg, du))

@@ -87,22 +87,27 @@ def run_rank(rank: int, world: int, cfg_dict: dict, method: int, backend: str, p
         start_step = load_checkpoint(eng, opts["resume"])
     data = make_data(cfg.data, cfg.tokens, cfg.model.D, cfg.torch_dtype, device)
     timer = StepTimer(device)
+    stop_after = int(opts.get("stop_after") or len(my_seeds))
+    done = start_step
     with maybe_profile(opts.get("profile", ""), rank):
         for i, s in enumerate(my_seeds.tolist()):
             if i < start_step:
                 continue
+            if i >= stop_after:
+                break
             timer.start()
             x, dy = data.fill(int(s))
             eng.train_step(x, dy)
             timer.stop()
+            done = i + 1
     timer.finish()
     if opts.get("ckpt_dir"):
-        save_checkpoint(eng, opts["ckpt_dir"], step=len(my_seeds), fmt=opts.get("ckpt_format", "consolidated"),
+        save_checkpoint(eng, opts["ckpt_dir"], step=done, fmt=opts.get("ckpt_format", "consolidated"),
                         meta={"method": method, "seed": seed, "cfg": cfg_dict})
     full = eng.gather_full_params() if opts.get("return_params", True) else None
     rec = None
     if rank == 0:
-        steps = len(my_seeds) - start_step
+        steps = done - start_step
         rec = {
             "method": method, "name": METHODS[method], "world": world, "steps": steps,
             "step_ms": timer.step_ms, "steady_ms": timer.steady_ms,

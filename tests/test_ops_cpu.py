@@ -1,0 +1,117 @@
+"""CPU checks of the op layer (torch reference path) and helpers."""
+import torch
+
+from dllm.models import reference as R
+from dllm.models.ffn import deinterleave_w13, init_ffn_layer, interleave_w13, layer_bwd, layer_fwd
+from dllm.ops.elementwise import _philox_normal_cpu, adam_step_, philox4x32_10, rng_normal_, sgd_step_
+from dllm.ops.gemm import _glu_merge, _glu_split, gemm
+from dllm.utils.config import ModelConfig, TrainConfig
+from dllm.utils.metrics import flops_per_step
+
+
+def test_philox_known_answers():
+    z = torch.zeros(1, dtype=torch.int64)
+    f = torch.full((1,), 0xFFFFFFFF, dtype=torch.int64)
+    assert [int(v) for v in philox4x32_10(z, z, z, z, 0, 0)] == [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]
+    assert [int(v) for v in philox4x32_10(f, f, f, f, 0xFFFFFFFF, 0xFFFFFFFF)] == [
+        0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD]
+
+
+def test_rng_deterministic_and_normal():
+    a = torch.empty(10_001)
+    b = torch.empty(10_001)
+    rng_normal_(a, seed=4, stream_id=2)
+    rng_normal_(b, seed=4, stream_id=2)
+    assert torch.equal(a, b)
+    c = torch.empty(10_001)
+    rng_normal_(c, seed=4, stream_id=3)
+    assert not torch.equal(a, c)
+    z = _philox_normal_cpu(1 << 18, 11, 0, 1.0)
+    assert abs(z.mean().item()) < 1e-2 and abs(z.std().item() - 1.0) < 1e-2
+
+
+def test_gemm_layouts_cpu():
+    a, b = torch.randn(6, 5), torch.randn(7, 5)
+    torch.testing.assert_close(gemm(a, b, "nt"), a @ b.t())
+    torch.testing.assert_close(gemm(a, b.t().contiguous(), "nn"), a @ b.t())
+    torch.testing.assert_close(gemm(a.t().contiguous(), b.t().contiguous(), "tn"), a @ b.t())
+    c = torch.ones(6, 7)
+    gemm(a, b, "nt", out=c, alpha=2.0, beta=1.0)
+    torch.testing.assert_close(c, 2 * a @ b.t() + 1)
+
+
+def test_glu_interleave_roundtrip():
+    w1, w3 = torch.randn(64, 8), torch.randn(64, 8)
+    w13 = interleave_w13(w1, w3)
+    assert torch.equal(w13[:16], w1[:16]) and torch.equal(w13[16:32], w3[:16])
+    r1, r3 = deinterleave_w13(w13)
+    assert torch.equal(r1, w1) and torch.equal(r3, w3)
+    h = torch.randn(3, 128)
+    g, u = _glu_split(h)
+    assert torch.equal(_glu_merge(g, u), h)
+
+
+def _layer_check(act, gated):
+    D, F, T = 16, 64, 32
+    gen = torch.Generator().manual_seed(0)
+    p = init_ffn_layer(D, F, gen, gated)
+    x, dy = torch.randn(T, D, dtype=torch.float64), torch.randn(T, D, dtype=torch.float64)
+    p = {k: v.double() for k, v in p.items()}
+    w1 = interleave_w13(p["w1"], p["w3"]) if gated else p["w1"]
+    R1 = w1.shape[0]
+    a = torch.empty(T, F, dtype=torch.float64)
+    h = torch.empty(T, R1, dtype=torch.float64)
+    y = torch.empty(T, D, dtype=torch.float64)
+    layer_fwd(x, w1, p["w2"], act, gated, a, h, y)
+    torch.testing.assert_close(y, R.layer_fwd(p, x, act))
+    gw1, gw2 = torch.empty_like(w1), torch.empty_like(p["w2"])
+    dx = layer_bwd(dy, x, w1, p["w2"], act, gated, a, h, gw1, gw2, torch.empty(T, R1, dtype=torch.float64),
+                   torch.empty(T, D, dtype=torch.float64))
+    rdx, rg = R.layer_bwd(dy, p, x, act)
+    torch.testing.assert_close(dx, rdx)
+    torch.testing.assert_close(gw2, rg["w2"])
+    if gated:
+        g1, g3 = deinterleave_w13(gw1)
+        torch.testing.assert_close(g1, rg["w1"])
+        torch.testing.assert_close(g3, rg["w3"])
+    else:
+        torch.testing.assert_close(gw1, rg["w1"])
+
+
+def test_layer_fwd_bwd_all_variants():
+    for act in ("relu", "silu", "gelu"):
+        for gated in (False, True):
+            _layer_check(act, gated)
+
+
+def test_autograd_agrees_with_reference_backward():
+    """Hand-written backward == torch autograd of the forward (fp64)."""
+    for act, gated in (("relu", False), ("gelu", False), ("silu", True)):
+        gen = torch.Generator().manual_seed(1)
+        p = {k: v.double().requires_grad_() for k, v in init_ffn_layer(8, 32, gen, gated).items()}
+        x = torch.randn(10, 8, dtype=torch.float64, requires_grad=True)
+        dy = torch.randn(10, 8, dtype=torch.float64)
+        y = R.layer_fwd(p, x, act)
+        y.backward(dy)
+        dx, g = R.layer_bwd(dy, {k: v.detach() for k, v in p.items()}, x.detach(), act)
+        torch.testing.assert_close(dx, x.grad)
+        for k in p:
+            torch.testing.assert_close(g[k], p[k].grad)
+
+
+def test_optimizers_cpu():
+    p, g = torch.randn(8), torch.randn(8)
+    q = p.clone()
+    sgd_step_(q, g, 0.1)
+    torch.testing.assert_close(q, p - 0.1 * g)
+    m, v = torch.zeros(8), torch.zeros(8)
+    q = p.clone()
+    adam_step_(q, g, m, v, 1, 0.01)
+    torch.testing.assert_close(q, p - 0.01 * g / (g.abs() + 1e-8), rtol=1e-5, atol=1e-6)
+
+
+def test_flops_accounting():
+    cfg = TrainConfig(model=ModelConfig(4096, 0, 8), batch_size=8, seq_len=1024)
+    unit = 2 * 8192 * 4096 * 16384
+    assert flops_per_step(cfg, recompute="full", skip_dx0=False) == 8 * 7 * unit  # reference: 7 GEMMs / layer
+    assert flops_per_step(cfg) == 8 * 6 * unit - unit
