@@ -294,6 +294,236 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_256(GemmArgs p) {
 }
 
 // ----------------------------------------------------------------------------------------------
+// bf16 256x256x64 MFMA kernel, 8-phase software pipeline (K % 128 == 0)
+//
+// LDS = 2 K-tile buffers x {A, B} x 2 half-tiles (16 KiB each: K-contiguous [128 rows][64 k], or
+// MN-contiguous [64 k][128 mn]) = 128 KiB.  One loop iteration = 2 K-tiles = 8 phases; in phase P
+// (buffer P/4, q = P%4) ALL waves compute block quadrant (QM,QN) = (0,0),(0,1),(1,1),(1,0)[q] — each
+// wave a 64x32 piece of it (8 waves = 2(M) x 4(N)), 16 MFMAs = 4x2 tiles x K 64.
+//   LDS reads : q0: A-half0 + B-half0, q1: B-half1, q2: A-half1, q3: none (B-half0 kept in registers)
+//   LDS-DMA   : one half-tile per phase, restaged >= 1 phase after its last read:
+//               P0 A1(odd,2i+1) P1 A0(even,2i+2) P2 B0(even) P3 B1(even) P4 A1(even)
+//               P5 A0(odd,2i+3) P6 B0(odd) P7 B1(odd)
+//   waits     : s_waitcnt vmcnt(6) (3 half-tiles left in flight) at P3 (retires the odd buffer, read in
+//               P4..P6) and P7 (retires the even buffer, read in P0..P2 of the next iteration);
+//               lgkmcnt(0) BEFORE the phase's first barrier, so a 1-phase restage distance is WAR-safe
+//               even with the optional one-interval stagger of waves 4-7 (the SIMD partners of waves
+//               0-3), which makes each SIMD alternate an MFMA segment with its partner's LDS segment.
+// Out-of-range prefetches of the last iteration are clamped to the last K-tile and land in slots that
+// are never read again, so every phase issues the same loads and the counted waits stay static.
+// ----------------------------------------------------------------------------------------------
+constexpr int HT = 16384;  // half-tile bytes
+
+__device__ __forceinline__ void kc_half_offsets(long ld, int wid, int lane, long off[2]) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int q = wid + 8 * i;  // piece 0..15: rows 8q..8q+7
+    const int row = 8 * q + (lane >> 3);
+    const int c = (lane & 7) ^ ((row >> 1) & 7);
+    off[i] = (long)row * ld + c * 8;
+  }
+}
+__device__ __forceinline__ void mc_half_offsets(long ld, int wid, int lane, long off[2]) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int q = wid + 8 * i;  // piece 0..15: k rows 4q..4q+3 of 256 B
+    const int krow = 4 * q + (lane >> 4);
+    const int u = (lane & 15) >> 1, h = lane & 1;
+    off[i] = (long)krow * ld + ((u ^ mc_swz(krow)) * 16) + h * 8;
+  }
+}
+// MN-contiguous half-tile fragment: rows of 256 B, 8 units of 32 B, unit XOR mc_swz(k) (3 bits)
+__device__ __forceinline__ bf16x8_t read_mc_half(const DLLM_LDS char* tile, int mn0, int kbase, int lane) {
+  const int i = lane & 15, q = i >> 2, p = i & 3;
+  const int k0 = kbase + q, k1 = kbase + 4 + q;
+  const int u = mn0 >> 4;
+  s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (DLLM_LDS s16x4_t*)(tile + k0 * 256 + ((u ^ mc_swz(k0)) << 5) + 8 * p));
+  s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (DLLM_LDS s16x4_t*)(tile + k1 * 256 + ((u ^ mc_swz(k1)) << 5) + 8 * p));
+  s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+#define DLLM_BARRIER()                      \
+  do {                                      \
+    asm volatile("" ::: "memory");          \
+    __builtin_amdgcn_s_barrier();           \
+    asm volatile("" ::: "memory");          \
+  } while (0)
+
+template <int LAYOUT, int EPI, typename OutT, bool STAGGER>
+__global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
+  __shared__ __attribute__((aligned(16))) char smem[8 * HT];  // slot (buf*2 + op)*2 + half
+  DLLM_LDS char* lds = (DLLM_LDS char*)smem;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  const int tiles_m = p.M / BT_M, tiles_n = p.N / BT_N;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int width = p.group_m * tiles_n;
+  const int first_m = (bid / width) * p.group_m;
+  const int gsz = min(tiles_m - first_m, p.group_m);
+  const int tm = first_m + (bid % width) % gsz;
+  const int tn = (bid % width) / gsz;
+  const int m0 = tm * BT_M, n0 = tn * BT_N;
+
+  constexpr bool A_KC = (LAYOUT != L_TN);
+  constexpr bool B_KC = (LAYOUT == L_NT);
+  const uint16_t* Ag = (const uint16_t*)p.A + (A_KC ? (long)m0 * p.lda : (long)m0);
+  const uint16_t* Bg = (const uint16_t*)p.B + (B_KC ? (long)n0 * p.ldb : (long)n0);
+  long aoff[2], boff[2];
+  if constexpr (A_KC) kc_half_offsets(p.lda, wid, lane, aoff); else mc_half_offsets(p.lda, wid, lane, aoff);
+  if constexpr (B_KC) kc_half_offsets(p.ldb, wid, lane, boff); else mc_half_offsets(p.ldb, wid, lane, boff);
+  const long a_kstep = A_KC ? BT_K : (long)BT_K * p.lda;
+  const long b_kstep = B_KC ? BT_K : (long)BT_K * p.ldb;
+  const long a_hstep = A_KC ? 128L * p.lda : 128L;
+  const long b_hstep = B_KC ? 128L * p.ldb : 128L;
+  const int nk = p.K / BT_K;  // even
+
+  // issue one half-tile (op 0 = A, 1 = B; half hh) of K-tile kt into buffer buf: 2 LDS-DMA per lane
+  auto stage = [&](int op, int hh, int kt, int buf) {
+    kt = min(kt, nk - 1);
+    DLLM_LDS char* dst = lds + ((buf * 2 + op) * 2 + hh) * HT;
+    const uint16_t* src = op == 0 ? Ag + kt * a_kstep + hh * a_hstep : Bg + kt * b_kstep + hh * b_hstep;
+    const long* off = op == 0 ? aoff : boff;
+    glds16(src + off[0], dst + wid * 1024);
+    glds16(src + off[1], dst + (wid + 8) * 1024);
+  };
+  auto slot = [&](int op, int hh, int buf) -> const DLLM_LDS char* {
+    return lds + ((buf * 2 + op) * 2 + hh) * HT;
+  };
+
+  f32x4_t acc[2][2][4][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int d = 0; d < 2; ++d) acc[a][b][c][d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8_t fa[4][2], fb0[2][2], fb1[2][2];  // [tile][k-substep]
+
+  auto read_a = [&](const DLLM_LDS char* t) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const int r0 = wr * 64 + mt * 16;
+        if constexpr (A_KC) fa[mt][s] = read_kc(t, r0 + (lane & 15), 4 * s + (lane >> 4));
+        else fa[mt][s] = read_mc_half(t, r0, 32 * s + 8 * (lane >> 4), lane);
+      }
+  };
+  auto read_b = [&](const DLLM_LDS char* t, bf16x8_t (&fb)[2][2]) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const int c0 = wc * 32 + nt * 16;
+        if constexpr (B_KC) fb[nt][s] = read_kc(t, c0 + (lane & 15), 4 * s + (lane >> 4));
+        else fb[nt][s] = read_mc_half(t, c0, 32 * s + 8 * (lane >> 4), lane);
+      }
+  };
+  auto mfma_quad = [&](f32x4_t (&c)[4][2], const bf16x8_t (&fb)[2][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+          c[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[nt][s], fa[mt][s], c[mt][nt], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // prologue: tile 0 -> even buffer (4 half-tiles), tile 1 -> odd (A0, B0, B1; A1 comes at P0)
+  stage(0, 0, 0, 0); stage(1, 0, 0, 0); stage(1, 1, 0, 0); stage(0, 1, 0, 0);
+  stage(0, 0, 1, 1); stage(1, 0, 1, 1); stage(1, 1, 1, 1);
+  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  DLLM_BARRIER();
+  if constexpr (STAGGER) {
+    if (wr == 1) DLLM_BARRIER();
+  }
+
+  for (int it = 0; it < nk / 2; ++it) {
+    const int te = 2 * it, to = 2 * it + 1;
+#define DLLM_PHASE_END(VMWAIT)                                       \
+  if (VMWAIT) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");       \
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                 \
+  DLLM_BARRIER();
+    // ---- even buffer (tile te) ----
+    read_a(slot(0, 0, 0)); read_b(slot(1, 0, 0), fb0);
+    stage(0, 1, to, 1);                        // P0: A1 odd
+    DLLM_PHASE_END(false)
+    mfma_quad(acc[0][0], fb0);
+    DLLM_BARRIER();
+    read_b(slot(1, 1, 0), fb1);
+    stage(0, 0, te + 2, 0);                    // P1: A0 even
+    DLLM_PHASE_END(false)
+    mfma_quad(acc[0][1], fb1);
+    DLLM_BARRIER();
+    read_a(slot(0, 1, 0));
+    stage(1, 0, te + 2, 0);                    // P2: B0 even
+    DLLM_PHASE_END(false)
+    mfma_quad(acc[1][1], fb1);
+    DLLM_BARRIER();
+    stage(1, 1, te + 2, 0);                    // P3: B1 even
+    DLLM_PHASE_END(true)
+    mfma_quad(acc[1][0], fb0);
+    DLLM_BARRIER();
+    // ---- odd buffer (tile to) ----
+    read_a(slot(0, 0, 1)); read_b(slot(1, 0, 1), fb0);
+    stage(0, 1, te + 2, 0);                    // P4: A1 even
+    DLLM_PHASE_END(false)
+    mfma_quad(acc[0][0], fb0);
+    DLLM_BARRIER();
+    read_b(slot(1, 1, 1), fb1);
+    stage(0, 0, to + 2, 1);                    // P5: A0 odd
+    DLLM_PHASE_END(false)
+    mfma_quad(acc[0][1], fb1);
+    DLLM_BARRIER();
+    read_a(slot(0, 1, 1));
+    stage(1, 0, to + 2, 1);                    // P6: B0 odd
+    DLLM_PHASE_END(false)
+    mfma_quad(acc[1][1], fb1);
+    DLLM_BARRIER();
+    stage(1, 1, to + 2, 1);                    // P7: B1 odd
+    DLLM_PHASE_END(true)
+    mfma_quad(acc[1][0], fb0);
+    DLLM_BARRIER();
+#undef DLLM_PHASE_END
+  }
+  if constexpr (STAGGER) {
+    if (wr == 0) DLLM_BARRIER();
+  }
+  // drain the clamped tail prefetches before the block can release its LDS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // epilogue: quadrant (QM,QN), tile (mt,nt): lane holds C[m][n..n+3]
+#pragma unroll
+  for (int QM = 0; QM < 2; ++QM)
+#pragma unroll
+    for (int QN = 0; QN < 2; ++QN)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const int m = m0 + QM * 128 + wr * 64 + mt * 16 + (lane & 15);
+        const int nb = n0 + QN * 128 + wc * 32 + 4 * (lane >> 4);
+        if constexpr (EPI == EPI_GLU) {
+          const int nc_out = (nb >> 5) * 16 + (nb & 15);
+          epi_glu_pair<OutT>(p, m, nc_out, nb, nb + 16, acc[QM][QN][mt][0], acc[QM][QN][mt][1]);
+        } else if constexpr (EPI == EPI_DGLU) {
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) epi_dglu<OutT>(p, m, nb + nt * 16, acc[QM][QN][mt][nt]);
+        } else {
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) epi4<EPI, OutT>(p, m, nb + nt * 16, acc[QM][QN][mt][nt]);
+        }
+      }
+}
+
+// ----------------------------------------------------------------------------------------------
 // fp32 128x128x16 MFMA kernel (exact fp32: v_mfma_f32_16x16x4_f32 is a k-ordered fmaf chain)
 // ----------------------------------------------------------------------------------------------
 constexpr int FT = 128, FK = 16, FLD = FT + 4;
@@ -485,13 +715,26 @@ __global__ void glu_combine(const T* h, long ldh, T* out, long ldo, int M, int F
 // ----------------------------------------------------------------------------------------------
 // host dispatch
 // ----------------------------------------------------------------------------------------------
+// variant: 0 = auto (8-phase when K % 128 == 0, else 2-stage), 1 = 2-stage, 2 = 8-phase, 3 = 8-phase staggered
+static int g_bf16_variant = 0;
+
 template <int L, int E>
 static hipError_t launch_bf16(const GemmArgs& a, int out_dt, hipStream_t s) {
   const int nb = (a.M / BT_M) * (a.N / BT_N);
-  if (out_dt == DT_F32)
-    hipLaunchKernelGGL((gemm_bf16_256<L, E, float>), dim3(nb), dim3(512), 0, s, a);
-  else
-    hipLaunchKernelGGL((gemm_bf16_256<L, E, uint16_t>), dim3(nb), dim3(512), 0, s, a);
+  int v = g_bf16_variant;
+  if (v == 0) v = (a.K % (2 * BT_K) == 0) ? 3 : 1;
+  if (v >= 2 && a.K % (2 * BT_K) != 0) v = 1;
+  const bool f32 = out_dt == DT_F32;
+  if (v == 1) {
+    if (f32) hipLaunchKernelGGL((gemm_bf16_256<L, E, float>), dim3(nb), dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((gemm_bf16_256<L, E, uint16_t>), dim3(nb), dim3(512), 0, s, a);
+  } else if (v == 2) {
+    if (f32) hipLaunchKernelGGL((gemm_bf16_8ph<L, E, float, false>), dim3(nb), dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((gemm_bf16_8ph<L, E, uint16_t, false>), dim3(nb), dim3(512), 0, s, a);
+  } else {
+    if (f32) hipLaunchKernelGGL((gemm_bf16_8ph<L, E, float, true>), dim3(nb), dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((gemm_bf16_8ph<L, E, uint16_t, true>), dim3(nb), dim3(512), 0, s, a);
+  }
   return hipGetLastError();
 }
 template <int L, int E>
@@ -580,6 +823,13 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
     e = hipGetLastError();
   }
   return (int)e;
+}
+
+// select the bf16 main-loop variant (see launch_bf16); returns the previous value
+int dllm_gemm_set_variant(int v) {
+  const int old = g_bf16_variant;
+  g_bf16_variant = v;
+  return old;
 }
 
 // which kernel family dllm_gemm would pick (for tests / profiling labels)

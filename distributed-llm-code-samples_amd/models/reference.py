@@ -89,6 +89,44 @@ def train_data_parallel(layers: list[dict], batches: list, n: int, lr: float, ac
     return ps
 
 
+def _q(t: torch.Tensor, dt) -> torch.Tensor:
+    return t if dt is None else t.to(dt).to(t.dtype)
+
+
+def stack_grads_mixed(layers: list[dict], x: torch.Tensor, dy: torch.Tensor, act: str = "relu",
+                      compute_dtype=torch.bfloat16):
+    """Oracle of the engine's mixed-precision dataflow (non-gated): weights, activations and activation
+    gradients rounded to ``compute_dtype`` exactly where the engine stores them; fp32 accumulation and
+    fp32 weight gradients (recompute='none')."""
+    q = lambda t: _q(t, compute_dtype)  # noqa: E731
+    w = [{k: q(v) for k, v in p.items()} for p in layers]
+    xs, hs, as_ = [q(x)], [], []
+    for p in w:
+        h = xs[-1] @ p["w1"].t()
+        hs.append(q(h))
+        as_.append(q(act_fwd(act, h)))
+        xs.append(q(as_[-1] @ p["w2"].t()))
+    grads = [None] * len(layers)
+    g = q(dy)
+    for i in reversed(range(len(layers))):
+        p = w[i]
+        gw2 = g.t() @ as_[i]
+        aux = as_[i] if act == "relu" else hs[i]
+        da = q((g @ p["w2"]) * act_grad(act, aux))
+        gw1 = da.t() @ xs[i]
+        grads[i] = {"w1": gw1, "w2": gw2}
+        g = q(da @ p["w1"])
+    return grads
+
+
+def train_single_mixed(layers, batches, lr, act="relu", compute_dtype=torch.bfloat16):
+    ps = _clone(layers)
+    for x, dy in batches:
+        grads = stack_grads_mixed(ps, x, dy, act, compute_dtype)
+        ps = [{k: p[k] - lr * g[k] for k in p} for p, g in zip(ps, grads)]
+    return ps
+
+
 def train_adam_single(layers, batches, lr, b1=0.9, b2=0.95, eps=1e-8, wd=0.0, act="relu"):
     ps = _clone(layers)
     m = [{k: torch.zeros_like(v) for k, v in p.items()} for p in ps]

@@ -143,6 +143,15 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
     return out
 
 
+BF16_VARIANTS = {"auto": 0, "2stage": 1, "8phase": 2, "8phase_stagger": 3}
+
+
+def set_bf16_variant(name: str) -> str:
+    """Select the bf16 256x256 main loop (process-wide); returns the previous setting's name."""
+    old = _native.lib().dllm_gemm_set_variant(BF16_VARIANTS[name])
+    return {v: k for k, v in BF16_VARIANTS.items()}[old]
+
+
 def gemm_path(a_dtype: torch.dtype, out_dtype: torch.dtype, M: int, N: int, K: int,
               lda: int, ldb: int, ldc: int) -> str:
     """Which native kernel family a call would use: 'mfma_bf16', 'mfma_f32' or 'generic'."""

@@ -1,0 +1,97 @@
+"""Per-GEMM throughput of the native gfx950 kernels vs torch.matmul (hipBLASLt) on the FFN shapes.
+
+    python scripts/bench_gemm.py [--T 8192 --D 4096 --F 16384] [--iters 20]
+
+Random N(0,1) bf16 operands (zero-filled operands read high on MI355X, guide §5.4 rule 25); variants are
+interleaved in one process (rule 24) and the median of the rounds is reported.
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import dllm  # noqa: E402,F401
+from dllm.ops.gemm import gemm, set_bf16_variant  # noqa: E402
+
+
+def timeit(fn, iters):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--T", type=int, default=8192)
+    ap.add_argument("--D", type=int, default=4096)
+    ap.add_argument("--F", type=int, default=16384)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--group_m", type=int, default=4)
+    ap.add_argument("--json", default="")
+    ap.add_argument("--variants", default="2stage,8phase,8phase_stagger")
+    a = ap.parse_args()
+    T, D, F = a.T, a.D, a.F
+    bf = torch.bfloat16
+    dev = "cuda"
+    x = torch.randn(T, D, device=dev, dtype=bf)
+    w1 = torch.randn(F, D, device=dev, dtype=bf) * 0.02
+    w2 = torch.randn(D, F, device=dev, dtype=bf) * 0.02
+    h = torch.randn(T, F, device=dev, dtype=bf)
+    act = torch.empty(T, F, device=dev, dtype=bf)
+    y = torch.empty(T, D, device=dev, dtype=bf)
+    dy = torch.randn(T, D, device=dev, dtype=bf)
+    da = torch.empty(T, F, device=dev, dtype=bf)
+    dx = torch.empty(T, D, device=dev, dtype=bf)
+    gw1 = torch.empty(F, D, device=dev, dtype=torch.float32)
+    gw2 = torch.empty(D, F, device=dev, dtype=torch.float32)
+    gm = a.group_m
+    cases = {
+        "fwd1 h=x.W1t (NT,act)": (lambda: gemm(x, w1, "nt", out=act, epi="act", act="relu", group_m=gm),
+                                  lambda: torch.relu(x @ w1.t())),
+        "fwd2 y=a.W2t (NT)": (lambda: gemm(h, w2, "nt", out=y, group_m=gm), lambda: h @ w2.t()),
+        "dW2=dyT.a (TN,f32)": (lambda: gemm(dy, h, "tn", out=gw2, group_m=gm),
+                               lambda: (dy.t() @ h).float()),
+        "da=dy.W2 (NN,dact)": (lambda: gemm(dy, w2, "nn", out=da, epi="dact", act="relu", aux=h, group_m=gm),
+                               lambda: (dy @ w2) * (h > 0)),
+        "dx=da.W1 (NN)": (lambda: gemm(h, w1, "nn", out=dx, group_m=gm), lambda: h @ w1),
+        "dW1=daT.x (TN,f32)": (lambda: gemm(h, x, "tn", out=gw1, group_m=gm), lambda: (h.t() @ x).float()),
+    }
+    flops = 2 * T * D * F
+    variants = a.variants.split(",")
+    res = {}
+    for name, (mine, ref) in cases.items():
+        times = {v: [] for v in variants}
+        tr = []
+        for _ in range(a.rounds):  # interleaved rounds in one process (guide §5.4 rule 24)
+            for v in variants:
+                set_bf16_variant(v)
+                times[v].append(timeit(mine, a.iters))
+            tr.append(timeit(ref, a.iters))
+        r = statistics.median(tr)
+        row = {"torch_ms": r, "torch_tflops": flops / r / 1e9}
+        msg = f"{name:26s} torch {flops / r / 1e9:7.1f} TF |"
+        for v in variants:
+            m = statistics.median(times[v])
+            row[v + "_ms"], row[v + "_tflops"] = m, flops / m / 1e9
+            msg += f" {v} {flops / m / 1e9:7.1f} TF"
+        res[name] = row
+        print(msg, flush=True)
+    set_bf16_variant("auto")
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump({"T": T, "D": D, "F": F, "cases": res}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

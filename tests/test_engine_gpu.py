@@ -23,7 +23,8 @@ def _setup(D, F, L, T, act, gated, steps, seed=5):
 @pytest.mark.parametrize("act,gated", [("relu", False), ("silu", False), ("gelu", False), ("silu", True)])
 @pytest.mark.parametrize("recompute", ["none", "full"])
 def test_fp32_engine_matches_oracle(act, gated, recompute):
-    D, F, L, T, lr = 128, 512, 2, 256, 1e-2
+    D, F, L, T = 128, 512, 2, 256
+    lr = 1.0 if gated else 1e-2  # gated updates are ~100x smaller at this init scale
     layers, batches = _setup(D, F, L, T, act, gated, 3)
     cfg = TrainConfig(model=ModelConfig(D, F, L, act, gated), batch_size=1, seq_len=T, dtype="fp32",
                       grad_dtype="fp32", lr=lr, recompute=recompute, skip_input_grad=False)
@@ -42,18 +43,39 @@ def test_fp32_engine_matches_oracle(act, gated, recompute):
             assert rel < 2e-3, (k, rel.item())
 
 
-@pytest.mark.parametrize("act,gated", [("relu", False), ("silu", True)])
-def test_bf16_engine_tracks_oracle(act, gated):
+@pytest.mark.parametrize("act", ["relu", "gelu"])
+def test_bf16_engine_matches_mixed_precision_oracle(act):
+    """bf16 compute + fp32 master/grad path vs an oracle that rounds at exactly the same points."""
     D, F, L, T, lr = 256, 1024, 2, 512, 1e-2
-    layers, batches = _setup(D, F, L, T, act, gated, 2)
-    cfg = TrainConfig(model=ModelConfig(D, F, L, act, gated), batch_size=1, seq_len=T, dtype="bf16",
+    layers, batches = _setup(D, F, L, T, act, False, 2)
+    cfg = TrainConfig(model=ModelConfig(D, F, L, act, False), batch_size=1, seq_len=T, dtype="bf16",
+                      grad_dtype="fp32", lr=lr, skip_input_grad=False)
+    eng = FFNTrainer(cfg, Mesh(), torch.device("cuda"))
+    eng.load_full_params(layers)
+    for x, dy in batches:
+        eng.train_step(x.cuda().bfloat16(), dy.cuda().bfloat16())
+    got = eng.gather_full_params()
+    want = R.train_single_mixed(layers, batches, lr, act)
+    for g, w, p0 in zip(got, want, layers):
+        for k in g:
+            d_got, d_want = g[k].double() - p0[k].double(), w[k].double() - p0[k].double()
+            rel = (d_got - d_want).norm() / d_want.norm()
+            # ReLU: 1-ulp bf16 differences of layer-0 outputs flip a few layer-1 masks (full-size error
+            # on those elements); per-layer exactness is asserted by test_layer_intermediates_gpu_vs_cpu
+            assert rel < (6e-2 if act == "relu" else 2e-2), (k, rel.item())
+
+
+def test_bf16_gated_engine_tracks_fp32_oracle():
+    D, F, L, T, lr = 256, 1024, 2, 512, 1.0
+    layers, batches = _setup(D, F, L, T, "silu", True, 2)
+    cfg = TrainConfig(model=ModelConfig(D, F, L, "silu", True), batch_size=1, seq_len=T, dtype="bf16",
                       grad_dtype="fp32", lr=lr)
     eng = FFNTrainer(cfg, Mesh(), torch.device("cuda"))
     eng.load_full_params(layers)
     for x, dy in batches:
         eng.train_step(x.cuda().bfloat16(), dy.cuda().bfloat16())
     got = eng.gather_full_params()
-    want = R.train_single(layers, [(x.bfloat16().float(), dy.bfloat16().float()) for x, dy in batches], lr, act)
+    want = R.train_single(layers, [(x.bfloat16().float(), dy.bfloat16().float()) for x, dy in batches], lr, "silu")
     for g, w, p0 in zip(got, want, layers):
         for k in g:
             d_got, d_want = g[k].double() - p0[k].double(), w[k].double() - p0[k].double()
@@ -75,3 +97,35 @@ def test_adam_engine_matches_oracle():
     for g, w in zip(got, want):
         for k in g:
             torch.testing.assert_close(g[k], w[k], rtol=1e-4, atol=2e-5)
+
+
+@pytest.mark.parametrize("act", ["relu", "gelu"])
+def test_layer_intermediates_gpu_vs_cpu(act):
+    """Every intermediate of one bf16 layer fwd/bwd (a, y, dW2, da, dx, dW1) on the HIP kernels matches the
+    CPU path on identical inputs to fp32-summation-order precision."""
+    from dllm.models.ffn import layer_bwd, layer_fwd
+
+    D, F, T = 256, 1024, 512
+    gen = torch.Generator().manual_seed(5)
+    p = init_ffn_layer(D, F, gen)
+    x = torch.randn(T, D, generator=gen).bfloat16()
+    dy = (0.1 * torch.randn(T, D, generator=gen)).bfloat16()
+    w1, w2 = p["w1"].bfloat16(), p["w2"].bfloat16()
+    res = {}
+    for dev in ("cpu", "cuda"):
+        X, DY, W1, W2 = x.to(dev), dy.to(dev), w1.to(dev), w2.to(dev)
+        a = torch.empty(T, F, dtype=torch.bfloat16, device=dev)
+        h = torch.empty(T, F, dtype=torch.bfloat16, device=dev) if act != "relu" else None
+        y = torch.empty(T, D, dtype=torch.bfloat16, device=dev)
+        layer_fwd(X, W1, W2, act, False, a, h, y)
+        gw1, gw2 = torch.empty(F, D, device=dev), torch.empty(D, F, device=dev)
+        da = torch.empty(T, F, dtype=torch.bfloat16, device=dev)
+        dx = torch.empty(T, D, dtype=torch.bfloat16, device=dev)
+        layer_bwd(DY, X, W1, W2, act, False, a, h, gw1, gw2, da, dx)
+        res[dev] = dict(a=a, y=y, gw1=gw1, gw2=gw2, da=da, dx=dx)
+    for k, want in res["cpu"].items():
+        got = res["cuda"][k].cpu().double()
+        rel = ((got - want.double()).norm() / want.double().norm()).item()
+        assert rel < 1e-3, (k, rel)
+    if act == "relu":
+        assert torch.equal(res["cuda"]["a"].cpu() > 0, res["cpu"]["a"] > 0)

@@ -9,7 +9,7 @@ import os
 import pytest
 import torch
 
-from dllm.ops.gemm import gemm, gemm_path
+from dllm.ops.gemm import gemm, gemm_path, set_bf16_variant
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -39,6 +39,13 @@ def _ref(a, b, layout):
     return {"nt": lambda: a @ b.t(), "nn": lambda: a @ b, "tn": lambda: a.t() @ b}[layout]()
 
 
+@pytest.fixture(params=["2stage", "8phase", "8phase_stagger"])
+def variant(request):
+    old = set_bf16_variant(request.param)
+    yield request.param
+    set_bf16_variant(old)
+
+
 def test_native_library_is_loaded():
     import dllm._native as nat
 
@@ -50,8 +57,9 @@ def test_native_library_is_loaded():
 
 
 @pytest.mark.parametrize("layout", ["nt", "nn", "tn"])
-@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 320), (768, 512, 1024)])
-def test_bf16_mfma_exact_integers(layout, M, N, K):
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 320), (768, 512, 1024), (512, 512, 128),
+                                   (1280, 768, 640)])
+def test_bf16_mfma_exact_integers(layout, M, N, K, variant):
     a, b = _operands(layout, M, N, K, torch.bfloat16, seed=M + N + K, integer=True)
     assert gemm_path(torch.bfloat16, torch.float32, M, N, K, a.stride(0), b.stride(0), N) == "mfma_bf16"
     out = gemm(a.to(DEV), b.to(DEV), layout, out_dtype=torch.float32, force="mfma_bf16")
@@ -60,7 +68,7 @@ def test_bf16_mfma_exact_integers(layout, M, N, K):
 
 
 @pytest.mark.parametrize("layout", ["nt", "nn", "tn"])
-def test_identity_asymmetric(layout):
+def test_identity_asymmetric(layout, variant):
     n = 256
     eye = torch.eye(n, dtype=torch.bfloat16)
     B = (torch.arange(n * n).reshape(n, n) % 7 - 3).to(torch.bfloat16) * torch.arange(1, n + 1).reshape(n, 1).remainder(5).to(torch.bfloat16)
@@ -71,7 +79,7 @@ def test_identity_asymmetric(layout):
 
 @pytest.mark.parametrize("layout", ["nt", "nn", "tn"])
 @pytest.mark.parametrize("out_dtype", [torch.bfloat16, torch.float32])
-def test_bf16_mfma_random(layout, out_dtype):
+def test_bf16_mfma_random(layout, out_dtype, variant):
     M, N, K = 512, 1024, 768
     a, b = _operands(layout, M, N, K, torch.bfloat16, seed=5)
     out = gemm(a.to(DEV), b.to(DEV), layout, out_dtype=out_dtype, force="mfma_bf16").cpu().double()
@@ -82,7 +90,7 @@ def test_bf16_mfma_random(layout, out_dtype):
 
 @pytest.mark.parametrize("act", ["relu", "silu", "gelu"])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-def test_epilogues_match_torch(act, dtype):
+def test_epilogues_match_torch(act, dtype, variant):
     M, N, K = 256, 512, 256
     force = "mfma_bf16" if dtype == torch.bfloat16 else "mfma_f32"
     x, w1 = _operands("nt", M, N, K, dtype, seed=11)
@@ -106,7 +114,7 @@ def test_epilogues_match_torch(act, dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-def test_gated_epilogues(dtype):
+def test_gated_epilogues(dtype, variant):
     M, N, K = 256, 512, 256  # N = 2F interleaved
     force = "mfma_bf16" if dtype == torch.bfloat16 else "mfma_f32"
     x, w13 = _operands("nt", M, N, K, dtype, seed=21)
