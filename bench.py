@@ -58,6 +58,8 @@ def parse():
     p.add_argument("--sequence_parallel", action="store_true")
     p.add_argument("--seed", type=int, default=1234)
     p.add_argument("--json_out", default="")
+    p.add_argument("--force_comm", action="store_true",
+                   help="exercise the RCCL DDP/FSDP path at N=1 (size-1 communicators, unfused optimizer)")
     return p.parse_args()
 
 
@@ -68,7 +70,9 @@ def main() -> int:
     n = a.gpus or world
     if n != world:
         raise SystemExit(f"--gpus {n} but WORLD_SIZE={world}: launch N>1 with torchrun")
-    if world > 1:
+    if world > 1 or a.force_comm:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
         init_distributed("nccl")
     else:
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
@@ -87,8 +91,8 @@ def main() -> int:
     cfg = TrainConfig(model=m, batch_size=a.batch_size, seq_len=a.seq_len, num_steps=a.steps, dtype=a.dtype,
                       grad_dtype=a.grad_dtype, optimizer=a.optimizer, dp_mode=dp_mode, dp=dp, tp=tp,
                       bucket_mb=a.bucket_mb, recompute=a.recompute, sequence_parallel=a.sequence_parallel,
-                      data="device")
-    mesh = Mesh.build(dp, tp)
+                      data="device", force_comm=a.force_comm)
+    mesh = Mesh.build(dp, tp, force=a.force_comm)
     eng = FFNTrainer(cfg, mesh, dev)
     from dllm.models.ffn import init_ffn_params_device
 
@@ -131,14 +135,16 @@ def main() -> int:
                    "optimizer": a.optimizer, "grad_dtype": a.grad_dtype, "master_weights": "fp32"},
         "tflops_per_gpu": round(tflops, 1), "finite": finite,
     }
+    if a.force_comm:
+        rec["note"] = "force_comm: DDP/FSDP collectives over size-1 RCCL communicators"
     if rank == 0:
         print(json.dumps(rec), flush=True)
         if a.json_out:
             with open(a.json_out, "w") as f:
                 json.dump(rec, f)
-    if world > 1:
-        import torch.distributed as dist
+    import torch.distributed as dist
 
+    if dist.is_initialized():
         dist.destroy_process_group()
     return 0
 

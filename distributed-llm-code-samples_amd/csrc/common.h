@@ -25,7 +25,10 @@ enum Layout : int { L_NT = 0, L_NN = 1, L_TN = 2 };
 //   EPI_DACT  : C = acc * act'(aux)                            dgrad + activation bwd mask (K5+K6)
 //   EPI_GLU   : gated: acc tiles of W1/W3 interleaved by 16 rows; C = act(h1)*h3; aux_out = [h1|h3]
 //   EPI_DGLU  : gated bwd: C(16-col interleaved [dh1|dh3]) from acc = da and aux = interleaved [h1|h3]
-enum Epi : int { EPI_STORE = 0, EPI_ACT = 1, EPI_DACT = 2, EPI_GLU = 3, EPI_DGLU = 4 };
+//   EPI_SGD   : weight-gradient GEMM fused with the SGD update: C (fp32 master) += -lr*alpha*acc,
+//               aux_out (bf16 working copy, nullable) = bf16(C)   (train_ffns.py:114,172 fused)
+//   EPI_ADAM  : same with AdamW (moments m/v share C's layout)
+enum Epi : int { EPI_STORE = 0, EPI_ACT = 1, EPI_DACT = 2, EPI_GLU = 3, EPI_DGLU = 4, EPI_SGD = 5, EPI_ADAM = 6 };
 enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_SILU = 2, ACT_GELU = 3 };
 
 __device__ __forceinline__ float bf2f(uint16_t v) {

@@ -185,6 +185,6 @@ int dllm_cast(const void* in, int in_dtype, void* out, int out_dtype, long n, vo
   return (int)hipGetLastError();
 }
 
-int dllm_abi_version() { return 1; }
+int dllm_abi_version() { return 2; }
 
 }  // extern "C"

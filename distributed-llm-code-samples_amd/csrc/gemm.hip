@@ -37,6 +37,10 @@ struct GemmArgs {
   float alpha, beta;
   int act;
   int group_m;
+  // fused optimizer epilogues
+  float lr, b1, b2, eps, wd, bc1, bc2;
+  float* opt_m;
+  float* opt_v;
 };
 
 // ----------------------------------------------------------------------------------------------
@@ -103,6 +107,26 @@ __device__ __forceinline__ void epi4(const GemmArgs& p, int m, int n, f32x4_t v)
     f32x4_t h = Vec4<OutT>::load(p.aux, (long)m * p.ldaux + n);
     for (int r = 0; r < 4; ++r) v[r] *= act_grad(p.act, h[r]);
     Vec4<OutT>::store(p.C, ci, v);
+  } else if constexpr (EPI == EPI_SGD) {
+    f32x4_t w = Vec4<float>::load(p.C, ci);
+    for (int r = 0; r < 4; ++r) w[r] = __fadd_rn(w[r], __fmul_rn(-p.lr, __fmul_rn(p.alpha, v[r])));
+    Vec4<float>::store(p.C, ci, w);
+    if (p.aux_out) Vec4<uint16_t>::store(p.aux_out, (long)m * p.ldaux + n, w);
+  } else if constexpr (EPI == EPI_ADAM) {
+    f32x4_t w = Vec4<float>::load(p.C, ci);
+    f32x4_t mm = Vec4<float>::load(p.opt_m, ci);
+    f32x4_t vv = Vec4<float>::load(p.opt_v, ci);
+    for (int r = 0; r < 4; ++r) {
+      const float g = p.alpha * v[r];
+      mm[r] = p.b1 * mm[r] + (1.f - p.b1) * g;
+      vv[r] = p.b2 * vv[r] + (1.f - p.b2) * g * g;
+      const float mh = mm[r] / p.bc1, vh = vv[r] / p.bc2;
+      w[r] = w[r] - p.lr * (mh / (sqrtf(vh) + p.eps) + p.wd * w[r]);
+    }
+    Vec4<float>::store(p.C, ci, w);
+    Vec4<float>::store(p.opt_m, ci, mm);
+    Vec4<float>::store(p.opt_v, ci, vv);
+    if (p.aux_out) Vec4<uint16_t>::store(p.aux_out, (long)m * p.ldaux + n, w);
   }
 }
 
@@ -695,6 +719,23 @@ __global__ __launch_bounds__(256) void gemm_generic(GemmArgs p) {
         const float u = ld1<OutT>(p.aux, (long)m * p.ldaux + nu);
         st1<OutT>(p.C, (long)m * p.ldc + nu, v * act_fwd(p.act, g));
         st1<OutT>(p.C, (long)m * p.ldc + ng, v * u * act_grad(p.act, g));
+      } else if constexpr (EPI == EPI_SGD) {
+        const long ci = (long)m * p.ldc + n;
+        float* W = (float*)p.C;
+        const float w = __fadd_rn(W[ci], __fmul_rn(-p.lr, __fmul_rn(p.alpha, v)));
+        W[ci] = w;
+        if (p.aux_out) st1<uint16_t>(p.aux_out, (long)m * p.ldaux + n, w);
+      } else if constexpr (EPI == EPI_ADAM) {
+        const long ci = (long)m * p.ldc + n;
+        float* W = (float*)p.C;
+        const float g = p.alpha * v;
+        const float mm = p.b1 * p.opt_m[ci] + (1.f - p.b1) * g;
+        const float vv = p.b2 * p.opt_v[ci] + (1.f - p.b2) * g * g;
+        const float w = W[ci] - p.lr * ((mm / p.bc1) / (sqrtf(vv / p.bc2) + p.eps) + p.wd * W[ci]);
+        W[ci] = w;
+        p.opt_m[ci] = mm;
+        p.opt_v[ci] = vv;
+        if (p.aux_out) st1<uint16_t>(p.aux_out, (long)m * p.ldaux + n, w);
       }
     }
   }
@@ -775,6 +816,24 @@ static hipError_t dispatch_epi(int path, int epi, const GemmArgs& a, int in_dt, 
 #undef DLLM_EPI_CASE
 }
 
+// weight-gradient GEMMs with a fused optimizer epilogue: TN layout, fp32 master output only
+template <int E>
+static hipError_t dispatch_opt(int path, const GemmArgs& a, int in_dt, hipStream_t s) {
+  if (path == 0) {
+    const int nb = (a.M / BT_M) * (a.N / BT_N);
+    if (a.K % (2 * BT_K) == 0 && g_bf16_variant != 1)
+      hipLaunchKernelGGL((gemm_bf16_8ph<L_TN, E, float, true>), dim3(nb), dim3(512), 0, s, a);
+    else
+      hipLaunchKernelGGL((gemm_bf16_256<L_TN, E, float>), dim3(nb), dim3(512), 0, s, a);
+    return hipGetLastError();
+  }
+  if (path == 1) return launch_f32<L_TN, E>(a, s);
+  dim3 grid((a.N + 63) / 64, (a.M + 63) / 64);
+  if (in_dt == DT_BF16) hipLaunchKernelGGL((gemm_generic<L_TN, E, uint16_t, float>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((gemm_generic<L_TN, E, float, float>), grid, dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
 }  // namespace dllm
 
 using namespace dllm;
@@ -785,7 +844,8 @@ extern "C" {
 // force_path: -1 auto, 0 bf16-256 tile kernel, 1 fp32-128 kernel, 2 generic kernel.
 int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const void* A, long lda,
               const void* B, long ldb, void* C, long ldc, const void* aux, void* aux_out, long ldaux,
-              int M, int N, int K, float alpha, float beta, int group_m, int force_path, void* stream) {
+              int M, int N, int K, float alpha, float beta, int group_m, int force_path, void* stream,
+              float lr, float b1, float b2, float eps, float wd, int step, float* opt_m, float* opt_v) {
   if (M <= 0 || N <= 0 || K <= 0) return -1;
   if (layout < 0 || layout > 2) return -1;
   if ((epi == EPI_GLU || epi == EPI_DGLU) && (N % 32) != 0) return -1;
@@ -794,6 +854,15 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
   a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.ldaux = ldaux;
   a.M = M; a.N = N; a.K = K; a.alpha = alpha; a.beta = beta; a.act = act;
   a.group_m = group_m > 0 ? group_m : 4;
+  a.lr = lr; a.b1 = b1; a.b2 = b2; a.eps = eps; a.wd = wd; a.opt_m = opt_m; a.opt_v = opt_v;
+  a.bc1 = 1.f; a.bc2 = 1.f;
+  const bool opt_epi = (epi == EPI_SGD || epi == EPI_ADAM);
+  if (opt_epi && (layout != L_TN || out_dtype != DT_F32)) return -1;
+  if (epi == EPI_ADAM) {
+    if (step < 1 || !opt_m || !opt_v) return -1;
+    a.bc1 = 1.f - powf(b1, (float)step);
+    a.bc2 = 1.f - powf(b2, (float)step);
+  }
   int path = 2;
   const bool aligned_lds = (lda % 8 == 0) && (ldb % 8 == 0) && (ldc % 4 == 0) && (ldaux % 4 == 0);
   if (in_dtype == DT_BF16 && M % BT_M == 0 && N % BT_N == 0 && K % BT_K == 0 && aligned_lds) path = 0;
@@ -806,6 +875,10 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
   if (path == 2 && epi == EPI_GLU && aux_out == nullptr) return -1;
   hipStream_t s = (hipStream_t)stream;
   hipError_t e;
+  if (opt_epi) {
+    e = epi == EPI_SGD ? dispatch_opt<EPI_SGD>(path, a, in_dtype, s) : dispatch_opt<EPI_ADAM>(path, a, in_dtype, s);
+    return (int)e;
+  }
   switch (layout) {
     case L_NT: e = dispatch_epi<L_NT>(path, epi, a, in_dtype, out_dtype, s); break;
     case L_NN: e = dispatch_epi<L_NN>(path, epi, a, in_dtype, out_dtype, s); break;

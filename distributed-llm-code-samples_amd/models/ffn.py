@@ -8,11 +8,12 @@ Reference semantics (train_ffns.py:35-94):
 * backward by hand: ``dW2 = dyᵀ·a``, ``da = (dy·W2)⊙act'(h)``, ``dW1 = daᵀ·x``, ``dx = da·W1``
   (``:61-70``); the reference recomputes ``h`` from the saved layer input (``recompute="full"`` here).
 
-MI355X design: each layer is 4 GEMMs in forward+backward order ``fwd1, fwd2 | dW2, da, dx, dW1``, every
+MI355X design: each layer is 6 GEMMs in forward+backward order ``fwd1, fwd2 | da, dW2, dx, dW1``, every
 elementwise op fused into a GEMM epilogue (activation into fwd1, activation-derivative mask into the
 ``da`` dgrad), so the only HBM traffic is GEMM operands.  With ``recompute="none"`` (default) the forward
 keeps ``a`` (and ``h`` for non-ReLU activations) so the backward runs 4 GEMMs instead of the reference's
-5 — 6·P·T model FLOPs instead of 7·P·T.  ReLU needs no ``h``: ``act'(h) = [a > 0]``.
+5 — 6·P·T model FLOPs instead of 7·P·T.  ReLU needs no ``h``: ``act'(h) = [a > 0]``.  Without a gradient
+collective (one GPU, pure TP) the SGD/AdamW update is fused into the two weight-gradient GEMMs.
 
 Gated (SwiGLU, Llama-3 FFN): ``a = act(x·W1ᵀ) ⊙ (x·W3ᵀ)``.  W1 and W3 are stored row-interleaved in
 16-row blocks as one ``W13 [2F, D]`` so a single GEMM produces both pre-activations and its epilogue
@@ -98,27 +99,33 @@ def layer_fwd(x: torch.Tensor, w1: torch.Tensor, w2: torch.Tensor, act: str, gat
 
 
 def layer_bwd(dy: torch.Tensor, x: torch.Tensor, w1: torch.Tensor, w2: torch.Tensor, act: str, gated: bool,
-              a: torch.Tensor, h: torch.Tensor | None, gw1: torch.Tensor, gw2: torch.Tensor,
-              da_buf: torch.Tensor, dx_out: torch.Tensor | None, hooks=None) -> torch.Tensor | None:
-    """Backward of one layer; writes weight grads into ``gw1``/``gw2`` (overwrite) and returns dx.
+              a: torch.Tensor, h: torch.Tensor | None, gw1, gw2, da_buf: torch.Tensor,
+              dx_out: torch.Tensor | None, hooks=None) -> torch.Tensor | None:
+    """Backward of one layer; returns dx.
 
-    Order ``dW2, da, dx, dW1`` so that (a) the W2 gradient is ready for its collective first and (b) a
-    TP input-grad all-reduce of ``dx`` overlaps the dW1 GEMM.  ``hooks`` may define ``after_w2``,
-    ``after_dx`` and ``after_w1`` callbacks (communication issue points).
+    ``gw1``/``gw2`` are either gradient tensors (overwritten) or dicts of ``gemm`` keyword arguments for the
+    weight-gradient GEMMs — e.g. ``{"out": master, "epi": "sgd", "lr": …, "aux_out": bf16_copy}`` to fuse
+    the optimizer update into the GEMM epilogue when no gradient collective is needed.
+
+    Order ``da, dW2, dx, dW1``: every dgrad that reads a weight runs before that weight's (possibly fused)
+    update, a TP all-reduce of ``dx`` overlaps the dW1 GEMM, and ``hooks`` (``after_w2``, ``after_dx``,
+    ``after_w1``) mark the points where gradient collectives can be issued.
     """
-    gemm(dy, a, "tn", out=gw2)                                        # dW2 = dyᵀ·a        [D, F]
-    if hooks is not None:
-        hooks.after_w2()
     if gated:
         gemm(dy, w2, "nn", out=da_buf, epi="dglu", act=act, aux=h)    # [dg|du] interleaved [T, 2F]
     else:
         gemm(dy, w2, "nn", out=da_buf, epi="dact", act=act, aux=h if h is not None else a)
+    kw2 = gw2 if isinstance(gw2, dict) else {"out": gw2}
+    gemm(dy, a, "tn", **kw2)                                          # dW2 = dyᵀ·a        [D, F]
+    if hooks is not None:
+        hooks.after_w2()
     dx = None
     if dx_out is not None:
         dx = gemm(da_buf, w1, "nn", out=dx_out)                       # dx = da·W1         [T, D]
         if hooks is not None:
             hooks.after_dx(dx)
-    gemm(da_buf, x, "tn", out=gw1)                                    # dW1 = daᵀ·x        [F, D]
+    kw1 = gw1 if isinstance(gw1, dict) else {"out": gw1}
+    gemm(da_buf, x, "tn", **kw1)                                      # dW1 = daᵀ·x        [F, D]
     if hooks is not None:
         hooks.after_w1()
     return dx

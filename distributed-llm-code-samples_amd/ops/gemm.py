@@ -15,6 +15,9 @@ followed by an epilogue:
   ``aux_out`` = interleaved pre-activations
 * ``"dglu"``:  gated backward; ``acc`` = ``da`` (N columns), ``aux`` = interleaved [g|u], ``C`` = interleaved
   [dg|du] (2N columns)
+* ``"sgd"``:   weight-gradient GEMM fused with the optimizer: ``C`` is the fp32 master weight, updated in place
+  ``C += -lr·alpha·acc`` (reference ``param.add_(-LR*grad)``), ``aux_out`` = its bf16 working copy
+* ``"adam"``:  same with fused AdamW; ``opt_m``/``opt_v`` share ``C``'s layout
 
 CUDA (HIP) tensors run the hand-written gfx950 kernels of ``csrc/gemm.hip``; CPU tensors run the torch
 reference below (used by the CPU/gloo tests and as the numerics oracle).  There is no silent fallback:
@@ -28,7 +31,7 @@ from .. import _native
 from .activations import act_code, act_fwd, act_grad
 
 LAYOUTS = {"nt": 0, "nn": 1, "tn": 2}
-EPIS = {"store": 0, "act": 1, "dact": 2, "glu": 3, "dglu": 4}
+EPIS = {"store": 0, "act": 1, "dact": 2, "glu": 3, "dglu": 4, "sgd": 5, "adam": 6}
 FORCE = {None: -1, "mfma_bf16": 0, "mfma_f32": 1, "generic": 2}
 
 
@@ -71,7 +74,7 @@ def _glu_merge(g: torch.Tensor, u: torch.Tensor) -> torch.Tensor:
     return torch.stack([g.reshape(M, F // 16, 16), u.reshape(M, F // 16, 16)], dim=2).reshape(M, 2 * F)
 
 
-def _torch_gemm(a, b, layout, out, epi, act, aux, aux_out, alpha, beta):
+def _torch_gemm(a, b, layout, out, epi, act, aux, aux_out, alpha, beta, opt=None):
     acc_dt = torch.promote_types(a.dtype, torch.float32)  # fp32 accumulation (fp64 stays fp64 for oracles)
     af, bf = a.to(acc_dt), b.to(acc_dt)
     if layout == "nt":
@@ -101,13 +104,29 @@ def _torch_gemm(a, b, layout, out, epi, act, aux, aux_out, alpha, beta):
         du = acc * act_fwd(act, g)
         dg = acc * u * act_grad(act, g)
         out.copy_(_glu_merge(dg, du))
+    elif epi == "sgd":
+        out.add_(-opt["lr"] * (alpha * acc).to(out.dtype))
+        if aux_out is not None:
+            aux_out.copy_(out)
+    elif epi == "adam":
+        g = (alpha * acc).to(out.dtype)
+        b1, b2, step = opt["b1"], opt["b2"], opt["step"]
+        m, v = opt["m"], opt["v"]
+        m.mul_(b1).add_((1 - b1) * g)
+        v.mul_(b2).add_((1 - b2) * g * g)
+        upd = (m / (1 - b1 ** step)) / (torch.sqrt(v / (1 - b2 ** step)) + opt["eps"]) + opt["wd"] * out
+        out.sub_(opt["lr"] * upd)
+        if aux_out is not None:
+            aux_out.copy_(out)
     return out
 
 
 def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None = None, *, epi: str = "store",
          act: str = "none", aux: torch.Tensor | None = None, aux_out: torch.Tensor | None = None,
          alpha: float = 1.0, beta: float = 0.0, out_dtype: torch.dtype | None = None, group_m: int = 4,
-         force: str | None = None) -> torch.Tensor:
+         force: str | None = None, lr: float = 0.0, betas: tuple = (0.9, 0.95), eps: float = 1e-8,
+         wd: float = 0.0, step: int = 0, opt_m: torch.Tensor | None = None,
+         opt_v: torch.Tensor | None = None) -> torch.Tensor:
     M, N, K = gemm_shape(a, b, layout)
     if a.dtype != b.dtype:
         raise TypeError(f"gemm operands differ in dtype: {a.dtype} vs {b.dtype}")
@@ -120,15 +139,27 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
         raise ValueError(f"epilogue {epi} needs aux (pre-activation)")
     if epi == "glu" and N % 32:
         raise ValueError("gated GEMM needs N % 32 == 0 (16-row interleave)")
+    if epi in ("sgd", "adam"):
+        if layout != "tn" or out.dtype != torch.float32:
+            raise ValueError("fused-optimizer epilogues need the TN (weight-gradient) layout and an fp32 master")
+        if epi == "adam" and (opt_m is None or opt_v is None or step < 1):
+            raise ValueError("adam epilogue needs opt_m, opt_v and step >= 1")
+        for t in (opt_m, opt_v):
+            if t is not None and (t.shape != out.shape or t.stride() != out.stride()):
+                raise ValueError("optimizer moments must share the master weight's layout")
     if a.device.type != "cuda":
-        return _torch_gemm(a, b, layout, out, epi, act, aux, aux_out, alpha, beta)
+        opt = {"lr": lr, "b1": betas[0], "b2": betas[1], "eps": eps, "wd": wd, "step": step, "m": opt_m, "v": opt_v}
+        return _torch_gemm(a, b, layout, out, epi, act, aux, aux_out, alpha, beta, opt)
 
     for t, nm in ((a, "a"), (b, "b"), (out, "out")):
         _check_rowmajor(t, nm)
     auxt = aux if aux is not None else aux_out
     if auxt is not None:
         _check_rowmajor(auxt, "aux")
-        if auxt.dtype != out.dtype:
+        if epi in ("sgd", "adam"):
+            if auxt.dtype != torch.bfloat16 or auxt.shape != out.shape:
+                raise TypeError("fused-optimizer aux_out must be the bf16 copy of the master weight")
+        elif auxt.dtype != out.dtype:
             raise TypeError("aux / aux_out must have the output dtype")
     L = _native.lib()
     in_dt, out_dt = _native.dtype_code(a.dtype), _native.dtype_code(out.dtype)
@@ -138,7 +169,9 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
                      aux_out.data_ptr() if aux_out is not None else None,
                      auxt.stride(0) if auxt is not None else 0,
                      M, N, K, float(alpha), float(beta), int(group_m), FORCE[force],
-                     _native.stream_ptr(a.device))
+                     _native.stream_ptr(a.device), float(lr), float(betas[0]), float(betas[1]), float(eps),
+                     float(wd), int(step), opt_m.data_ptr() if opt_m is not None else None,
+                     opt_v.data_ptr() if opt_v is not None else None)
     _native.check(rc, f"dllm_gemm({layout},{epi},M={M},N={N},K={K})")
     return out
 

@@ -30,25 +30,25 @@ class Done:
         return True
 
 
-def _size(group) -> int:
-    if group is None or not dist.is_initialized():
-        return 1
-    return dist.get_world_size(group)
+def _active(group) -> bool:
+    """A collective on ``None`` (a mesh axis of size 1 without a communicator) is a local no-op; a real
+    group — even of size 1 (``Mesh.build(force=True)``) — always goes through the backend."""
+    return group is not None and dist.is_initialized()
 
 
 def all_reduce(t: torch.Tensor, group, async_op: bool = True):
-    if _size(group) == 1:
+    if not _active(group):
         return Done()
     w = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
     return w if async_op else Done()
 
 
 def all_gather_into(out: torch.Tensor, shard: torch.Tensor, group, async_op: bool = True):
-    n = _size(group)
-    if n == 1:
+    if not _active(group):
         if out.data_ptr() != shard.data_ptr():
             out.copy_(shard.view_as(out))
         return Done()
+    n = dist.get_world_size(group)
     if out.numel() != shard.numel() * n:
         raise ValueError(f"all_gather_into: out {out.numel()} != {n} x shard {shard.numel()}")
     w = dist.all_gather_into_tensor(out.view(-1), shard.reshape(-1), group=group, async_op=async_op)
@@ -56,11 +56,11 @@ def all_gather_into(out: torch.Tensor, shard: torch.Tensor, group, async_op: boo
 
 
 def reduce_scatter_into(out: torch.Tensor, full: torch.Tensor, group, async_op: bool = True):
-    n = _size(group)
-    if n == 1:
+    if not _active(group):
         if out.data_ptr() != full.data_ptr():
             out.copy_(full.view_as(out))
         return Done()
+    n = dist.get_world_size(group)
     if full.numel() != out.numel() * n:
         raise ValueError(f"reduce_scatter_into: full {full.numel()} != {n} x out {out.numel()}")
     w = dist.reduce_scatter_tensor(out.view(-1), full.reshape(-1), op=dist.ReduceOp.SUM, group=group,
@@ -70,9 +70,9 @@ def reduce_scatter_into(out: torch.Tensor, full: torch.Tensor, group, async_op: 
 
 def gather_to_rank0(t: torch.Tensor, group=None) -> list[torch.Tensor] | None:
     """Gather equally-shaped tensors from every rank of ``group`` onto rank 0 of that group (CPU copies)."""
-    n = _size(group)
-    if n == 1:
+    if group is None or not dist.is_initialized() or dist.get_world_size(group) == 1:
         return [t.detach().cpu()]
+    n = dist.get_world_size(group)
     outs = [torch.empty_like(t) for _ in range(n)]
     dist.all_gather(outs, t.contiguous(), group=group)
     return [o.cpu() for o in outs]

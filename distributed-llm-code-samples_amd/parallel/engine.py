@@ -106,8 +106,9 @@ class FFNTrainer:
         if self.gated and self.F_loc % 16:
             raise ValueError("gated FFN needs (F / tp) % 16 == 0")
         self.R1 = (2 if self.gated else 1) * self.F_loc
-        self.fsdp = cfg.dp_mode == "fsdp" and d > 1
-        self.ddp = cfg.dp_mode in ("ddp", "fsdp") and d > 1 and not self.fsdp
+        multi = d > 1 or cfg.force_comm
+        self.fsdp = cfg.dp_mode == "fsdp" and multi
+        self.ddp = cfg.dp_mode == "ddp" and multi
         if d > 1 and cfg.dp_mode == "none":
             raise ValueError("dp > 1 needs dp_mode ddp or fsdp")
         if self.fsdp and (self.R1 % d or D % d):
@@ -137,7 +138,10 @@ class FFNTrainer:
         self.master = torch.zeros(self.total, dtype=torch.float32, device=dev)
         self.shared_copy = self.cd == torch.float32
         self.copy = self.master if self.shared_copy else torch.zeros(self.total, dtype=self.cd, device=dev)
-        self.grads = torch.zeros(self.total, dtype=self.gd, device=dev)
+        # no gradient collective (single device / pure TP): the optimizer runs inside the wgrad GEMMs and
+        # no flat gradient buffer exists at all
+        self.fused_opt = cfg.fused_optimizer and not (self.ddp or self.fsdp)
+        self.grads = torch.zeros(0 if self.fused_opt else self.total, dtype=self.gd, device=dev)
         if cfg.optimizer == "adam":
             self.adam_m = torch.zeros(self.total, dtype=torch.float32, device=dev)
             self.adam_v = torch.zeros(self.total, dtype=torch.float32, device=dev)
@@ -279,6 +283,17 @@ class FFNTrainer:
     # ------------------------------------------------------------------------------------------------
     # optimizer over a flat range
     # ------------------------------------------------------------------------------------------------
+    def _fused_wgrad_kw(self, l: int, name: str) -> dict:
+        cfg = self.cfg
+        kw = {"out": self.master_view(l, name), "epi": cfg.optimizer, "lr": cfg.lr}
+        if not self.shared_copy:
+            kw["aux_out"] = self.copy_view(l, name)
+        if cfg.optimizer == "adam":
+            e = self.entry[(l, name)]
+            kw.update(betas=(cfg.adam_b1, cfg.adam_b2), eps=cfg.adam_eps, wd=cfg.weight_decay, step=self.step_count,
+                      opt_m=self._view(self.adam_m, e), opt_v=self._view(self.adam_v, e))
+        return kw
+
     def _opt(self, s: int, e: int) -> None:
         cfg = self.cfg
         master, grad = self.master[s:e], self.grads[s:e]
@@ -396,6 +411,9 @@ class FFNTrainer:
                 slot = l % 2
                 self._fsdp_finish_rs(slot)  # slot's previous grads (layer l+2) must be reduced first
                 gw1, gw2 = self.gring[slot]["w1"], self.gring[slot]["w2"]
+            elif self.fused_opt:
+                w1, w2 = self.copy_view(l, "w1"), self.copy_view(l, "w2")
+                gw1, gw2 = self._fused_wgrad_kw(l, "w1"), self._fused_wgrad_kw(l, "w2")
             else:
                 w1, w2 = self.copy_view(l, "w1"), self.copy_view(l, "w2")
                 gw1, gw2 = self.grad_view(l, "w1"), self.grad_view(l, "w2")
@@ -437,7 +455,7 @@ class FFNTrainer:
         elif self.fsdp:
             for slot in ((L - 1) % 2, L % 2):
                 self._fsdp_finish_rs(slot)
-        else:
+        elif not self.fused_opt:
             self._opt(0, self.total)
         return y
 

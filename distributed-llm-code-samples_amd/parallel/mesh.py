@@ -77,8 +77,11 @@ class Mesh:
         return self.groups.get(role)
 
     @classmethod
-    def build(cls, dp: int, tp: int, separate_streams: bool = True) -> "Mesh":
-        """Create the role process groups (collective: every rank must call it with the same args)."""
+    def build(cls, dp: int, tp: int, separate_streams: bool = True, force: bool = False) -> "Mesh":
+        """Create the role process groups (collective: every rank must call it with the same args).
+
+        ``force`` also creates groups for axes of size 1 (used to exercise the RCCL code paths with a
+        single GPU: a size-1 communicator still runs real collectives and stream waits)."""
         world = dist.get_world_size() if dist.is_initialized() else 1
         rank = dist.get_rank() if dist.is_initialized() else 0
         if dp * tp != world:
@@ -86,12 +89,12 @@ class Mesh:
         m = cls(dp=dp, tp=tp, rank=rank)
         m.dp_ranks = [d * tp + m.tp_rank for d in range(dp)]
         m.tp_ranks = [m.dp_rank * tp + t for t in range(tp)]
-        if world == 1 or not dist.is_initialized():
+        if not dist.is_initialized() or (world == 1 and not force):
             return m
         # every rank creates every group in the same order (new_group is collective)
         for role in ROLES:
             if role.startswith("dp"):
-                if dp == 1:
+                if dp == 1 and not force:
                     continue
                 if not separate_streams and role != "dp_ar" and "dp_ar" in m.groups:
                     m.groups[role] = m.groups["dp_ar"]
@@ -108,7 +111,7 @@ class Mesh:
                             mine = g
                     m.groups[role] = mine
             else:
-                if tp == 1:
+                if tp == 1 and not force:
                     continue
                 if tp == world:
                     m.groups[role] = dist.new_group(list(range(world)))

@@ -64,6 +64,8 @@ class TrainConfig:
     skip_input_grad: bool = True     # layer-0 dx is never consumed (reference computes it, :68)
     separate_streams: bool = True    # one communicator/stream per comm role
     tp_overlap: bool = True          # overlap the TP dx all-reduce with the dW1 GEMM
+    fused_optimizer: bool = True     # fuse SGD/Adam into the wgrad GEMM epilogue when no grad collective
+    force_comm: bool = False         # run the DDP/FSDP collective path even at dp=1 (single-GPU RCCL check)
 
     @property
     def tokens(self) -> int:

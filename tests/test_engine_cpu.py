@@ -10,12 +10,12 @@ from dllm.utils.config import ModelConfig, TrainConfig
 from dllm.utils.data import reference_mock_data
 
 
-def _run(act, gated, recompute, opt="sgd", lr=1e-2, steps=3, D=16, F=64, L=3, T=32):
+def _run(act, gated, recompute, opt="sgd", lr=1e-2, steps=3, D=16, F=64, L=3, T=32, fused=True):
     gen = torch.Generator().manual_seed(3)
     layers = [init_ffn_layer(D, F, gen, gated) for _ in range(L)]
     batches = list(reference_mock_data(torch.randint(100_000, (steps,), generator=gen), T, D))
     cfg = TrainConfig(model=ModelConfig(D, F, L, act, gated), batch_size=1, seq_len=T, lr=lr, optimizer=opt,
-                      recompute=recompute)
+                      recompute=recompute, fused_optimizer=fused)
     eng = FFNTrainer(cfg, Mesh(), torch.device("cpu"))
     eng.load_full_params(layers)
     for x, dy in batches:
@@ -56,3 +56,12 @@ def test_bf16_compute_on_cpu_tracks_fp32():
         for k in w:
             rel = ((g[k] - p[k]) - (w[k] - p[k])).norm() / (w[k] - p[k]).norm()
             assert rel < 1e-1, (k, rel.item())  # bf16 activations + ReLU-mask flips at tiny T
+
+
+@pytest.mark.parametrize("opt", ["sgd", "adam"])
+def test_fused_optimizer_equals_unfused(opt):
+    a, _, _ = _run("silu", True, "none", opt=opt, lr=1e-3, fused=True)
+    b, _, _ = _run("silu", True, "none", opt=opt, lr=1e-3, fused=False)
+    for g, w in zip(a, b):
+        for k in w:
+            torch.testing.assert_close(g[k], w[k], rtol=1e-6, atol=1e-8)

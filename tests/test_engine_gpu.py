@@ -129,3 +129,24 @@ def test_layer_intermediates_gpu_vs_cpu(act):
         assert rel < 1e-3, (k, rel)
     if act == "relu":
         assert torch.equal(res["cuda"]["a"].cpu() > 0, res["cpu"]["a"] > 0)
+
+
+@pytest.mark.parametrize("opt", ["sgd", "adam"])
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_fused_optimizer_epilogue_matches_separate_kernel(opt, dtype):
+    D, F, L, T = 256, 1024, 2, 512
+    layers, batches = _setup(D, F, L, T, "relu", False, 2)
+    out = []
+    for fused in (True, False):
+        cfg = TrainConfig(model=ModelConfig(D, F, L), batch_size=1, seq_len=T, dtype=dtype, grad_dtype="fp32",
+                          lr=1e-3, optimizer=opt, fused_optimizer=fused)
+        eng = FFNTrainer(cfg, Mesh(), torch.device("cuda"))
+        eng.load_full_params(layers)
+        cd = torch.bfloat16 if dtype == "bf16" else torch.float32
+        for x, dy in batches:
+            eng.train_step(x.cuda().to(cd), dy.cuda().to(cd))
+        out.append(eng.gather_full_params())
+        assert eng.fused_opt == fused
+    for g, w in zip(*out):
+        for k in w:
+            torch.testing.assert_close(g[k], w[k], rtol=1e-5, atol=1e-6)
