@@ -22,6 +22,8 @@
 //    raster so blocks sharing operand panels run on one XCD's L2.
 //  * gemm_f32_128: exact-fp32 parity path (mfma_f32_16x16x4f32), 128x128x16 tile, register-staged.
 //  * gemm_generic: any shape / any dtype, bounds-checked FMA kernel (tests, odd TP shards).
+#include <type_traits>
+
 #include "common.h"
 
 namespace dllm {
@@ -376,9 +378,41 @@ __device__ __forceinline__ bf16x8_t read_mc_half(const DLLM_LDS char* tile, int 
     asm volatile("" ::: "memory");          \
   } while (0)
 
-template <int LAYOUT, int EPI, typename OutT, bool STAGGER>
+// ABL (ablation builds only; 0 in production): bit0/1 force K-contiguous LOADS of A/B, bit2/3 force
+// K-contiguous fragment READS of A/B, independent of LAYOUT (wrong results, same work) -- isolates the
+// cost of MN-contiguous LDS-DMA patterns vs transposed ds_read_b64_tr_b16 fragment reads.
+// Fragment reads of the 8-phase kernel are inline asm: hipcc cannot prove that a ds_read does not
+// alias an in-flight LDS-DMA (global_load_lds) write and would drain the whole prefetch pipeline with
+// s_waitcnt vmcnt(0) before every phase's reads.  RAW/WAR ordering against the DMA is instead carried
+// by the counted vmcnt + barrier schedule below, and each phase ends its reads with an explicit
+// lgkmcnt(0) + sched_barrier(0) before any MFMA consumes them (cdna_hip_programming.md §5.4 rule 18,
+// §5.7 item 1 form (iii)).  Addresses are per-lane base VGPRs + compile-time offset immediates.
+template <int OFF>
+__device__ __forceinline__ void lds_b128(bf16x8_t& d, uint32_t addr) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(addr), "i"(OFF));
+}
+template <int OFF>
+__device__ __forceinline__ void lds_tr16(s16x4_t& d, uint32_t addr) {
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(d) : "v"(addr), "i"(OFF));
+}
+__device__ __forceinline__ bf16x8_t cat_tr(s16x4_t lo, s16x4_t hi) {
+  s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+#define DLLM_LDS_WAIT()                                   \
+  do {                                                    \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");    \
+    __builtin_amdgcn_sched_barrier(0);                    \
+  } while (0)
+
+// ABL (ablation builds only; 0 in production): bit0/1 force K-contiguous LOADS of A/B, bit2/3 force
+// K-contiguous fragment READS of A/B, independent of LAYOUT (wrong results, same work) -- isolates the
+// cost of MN-contiguous LDS-DMA patterns vs transposed ds_read_b64_tr_b16 fragment reads.
+template <int LAYOUT, int EPI, typename OutT, bool STAGGER, int ABL = 0>
 __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
-  __shared__ __attribute__((aligned(16))) char smem[8 * HT];  // slot (buf*2 + op)*2 + half
+  // slot(op, hh, buf) = ((op*2 + hh)*2 + buf) * 16 KiB: A in [0, 64K), B in [64K, 128K), so every
+  // fragment read is base + a 16-bit immediate
+  __shared__ __attribute__((aligned(16))) char smem[8 * HT];
   DLLM_LDS char* lds = (DLLM_LDS char*)smem;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -392,8 +426,10 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
   const int tn = (bid % width) / gsz;
   const int m0 = tm * BT_M, n0 = tn * BT_N;
 
-  constexpr bool A_KC = (LAYOUT != L_TN);
-  constexpr bool B_KC = (LAYOUT == L_NT);
+  constexpr bool A_KC = (ABL & 1) ? true : (LAYOUT != L_TN);
+  constexpr bool B_KC = (ABL & 2) ? true : (LAYOUT == L_NT);
+  constexpr bool A_RKC = (ABL & 4) ? true : (LAYOUT != L_TN);
+  constexpr bool B_RKC = (ABL & 8) ? true : (LAYOUT == L_NT);
   const uint16_t* Ag = (const uint16_t*)p.A + (A_KC ? (long)m0 * p.lda : (long)m0);
   const uint16_t* Bg = (const uint16_t*)p.B + (B_KC ? (long)n0 * p.ldb : (long)n0);
   long aoff[2], boff[2];
@@ -405,18 +441,39 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
   const long b_hstep = B_KC ? 128L * p.ldb : 128L;
   const int nk = p.K / BT_K;  // even
 
-  // issue one half-tile (op 0 = A, 1 = B; half hh) of K-tile kt into buffer buf: 2 LDS-DMA per lane
   auto stage = [&](int op, int hh, int kt, int buf) {
     kt = min(kt, nk - 1);
-    DLLM_LDS char* dst = lds + ((buf * 2 + op) * 2 + hh) * HT;
+    DLLM_LDS char* dst = lds + ((op * 2 + hh) * 2 + buf) * HT;
     const uint16_t* src = op == 0 ? Ag + kt * a_kstep + hh * a_hstep : Bg + kt * b_kstep + hh * b_hstep;
     const long* off = op == 0 ? aoff : boff;
     glds16(src + off[0], dst + wid * 1024);
     glds16(src + off[1], dst + (wid + 8) * 1024);
   };
-  auto slot = [&](int op, int hh, int buf) -> const DLLM_LDS char* {
-    return lds + ((buf * 2 + op) * 2 + hh) * HT;
-  };
+
+  // ---- per-lane fragment base addresses (LDS byte addresses) ----
+  const uint32_t lds_base = (uint32_t)(uintptr_t)lds;
+  const int g = lane >> 4, i15 = lane & 15;
+  // K-contiguous image (128-B rows, chunk ^= (row>>1)&7): base for k-substep s; rows R + mt*16 + i15
+  const int fkc = (i15 >> 1) & 7;
+  // MN-contiguous image (256-B rows, unit ^= (k&3)|((k>>3)&1)<<2): per tile t
+  const int q = i15 >> 2, pp = i15 & 3, swz = q | ((g & 1) << 2);
+  uint32_t abase[4], bbase[2];
+  if constexpr (A_RKC) {
+    abase[0] = lds_base + (wr * 64 + i15) * 128 + (((0 + g) ^ fkc) << 4);
+    abase[1] = lds_base + (wr * 64 + i15) * 128 + (((4 + g) ^ fkc) << 4);
+  } else {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      abase[t] = lds_base + (8 * g + q) * 256 + (((4 * wr + t) ^ swz) << 5) + 8 * pp;
+  }
+  if constexpr (B_RKC) {
+    bbase[0] = lds_base + 4 * HT + (wc * 32 + i15) * 128 + (((0 + g) ^ fkc) << 4);
+    bbase[1] = lds_base + 4 * HT + (wc * 32 + i15) * 128 + (((4 + g) ^ fkc) << 4);
+  } else {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+      bbase[t] = lds_base + 4 * HT + (8 * g + q) * 256 + (((2 * wc + t) ^ swz) << 5) + 8 * pp;
+  }
 
   f32x4_t acc[2][2][4][2];
 #pragma unroll
@@ -429,38 +486,68 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
         for (int d = 0; d < 2; ++d) acc[a][b][c][d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   bf16x8_t fa[4][2], fb0[2][2], fb1[2][2];  // [tile][k-substep]
+  // transposed-read halves: issued in the read segment, combined after the phase's single lgkmcnt(0)
+  s16x4_t ta_lo[4][2], ta_hi[4][2], tb_lo[2][2], tb_hi[2][2];
 
-  auto read_a = [&](const DLLM_LDS char* t) {
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        const int r0 = wr * 64 + mt * 16;
-        if constexpr (A_KC) fa[mt][s] = read_kc(t, r0 + (lane & 15), 4 * s + (lane >> 4));
-        else fa[mt][s] = read_mc_half(t, r0, 32 * s + 8 * (lane >> 4), lane);
-      }
+  // A half hh of buffer buf -> fa ; B half hh of buffer buf -> fb   (issue only)
+  auto read_a = [&](auto hh_c, auto buf_c) {
+    constexpr int SO = (hh_c.value * 2 + buf_c.value) * HT;
+    if constexpr (A_RKC) {
+      lds_b128<SO + 0 * 2048>(fa[0][0], abase[0]); lds_b128<SO + 1 * 2048>(fa[1][0], abase[0]);
+      lds_b128<SO + 2 * 2048>(fa[2][0], abase[0]); lds_b128<SO + 3 * 2048>(fa[3][0], abase[0]);
+      lds_b128<SO + 0 * 2048>(fa[0][1], abase[1]); lds_b128<SO + 1 * 2048>(fa[1][1], abase[1]);
+      lds_b128<SO + 2 * 2048>(fa[2][1], abase[1]); lds_b128<SO + 3 * 2048>(fa[3][1], abase[1]);
+    } else {
+#define DLLM_TRA(t, s)                                              \
+  lds_tr16<SO + (s) * 8192>(ta_lo[t][s], abase[t]);                 \
+  lds_tr16<SO + (s) * 8192 + 1024>(ta_hi[t][s], abase[t]);
+      DLLM_TRA(0, 0) DLLM_TRA(1, 0) DLLM_TRA(2, 0) DLLM_TRA(3, 0)
+      DLLM_TRA(0, 1) DLLM_TRA(1, 1) DLLM_TRA(2, 1) DLLM_TRA(3, 1)
+#undef DLLM_TRA
+    }
   };
-  auto read_b = [&](const DLLM_LDS char* t, bf16x8_t (&fb)[2][2]) {
+  auto fin_a = [&]() {  // after the phase's lgkmcnt(0)
+    if constexpr (!A_RKC) {
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+      for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const int c0 = wc * 32 + nt * 16;
-        if constexpr (B_KC) fb[nt][s] = read_kc(t, c0 + (lane & 15), 4 * s + (lane >> 4));
-        else fb[nt][s] = read_mc_half(t, c0, 32 * s + 8 * (lane >> 4), lane);
-      }
+        for (int s2 = 0; s2 < 2; ++s2) fa[t][s2] = cat_tr(ta_lo[t][s2], ta_hi[t][s2]);
+    }
+  };
+  auto read_b = [&](auto hh_c, auto buf_c, bf16x8_t (&fb)[2][2]) {
+    constexpr int SO = (hh_c.value * 2 + buf_c.value) * HT;
+    if constexpr (B_RKC) {
+      lds_b128<SO + 0 * 2048>(fb[0][0], bbase[0]); lds_b128<SO + 1 * 2048>(fb[1][0], bbase[0]);
+      lds_b128<SO + 0 * 2048>(fb[0][1], bbase[1]); lds_b128<SO + 1 * 2048>(fb[1][1], bbase[1]);
+    } else {
+#define DLLM_TRB(t, s)                                              \
+  lds_tr16<SO + (s) * 8192>(tb_lo[t][s], bbase[t]);                 \
+  lds_tr16<SO + (s) * 8192 + 1024>(tb_hi[t][s], bbase[t]);
+      DLLM_TRB(0, 0) DLLM_TRB(1, 0) DLLM_TRB(0, 1) DLLM_TRB(1, 1)
+#undef DLLM_TRB
+    }
+  };
+  auto fin_b = [&](bf16x8_t (&fb)[2][2]) {
+    if constexpr (!B_RKC) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) fb[t][s2] = cat_tr(tb_lo[t][s2], tb_hi[t][s2]);
+    }
   };
   auto mfma_quad = [&](f32x4_t (&c)[4][2], const bf16x8_t (&fb)[2][2]) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+    for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt)
-          c[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[nt][s], fa[mt][s], c[mt][nt], 0, 0, 0);
+          c[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[nt][s2], fa[mt][s2], c[mt][nt], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
 
   // prologue: tile 0 -> even buffer (4 half-tiles), tile 1 -> odd (A0, B0, B1; A1 comes at P0)
   stage(0, 0, 0, 0); stage(1, 0, 0, 0); stage(1, 1, 0, 0); stage(0, 1, 0, 0);
@@ -475,22 +562,25 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
     const int te = 2 * it, to = 2 * it + 1;
 #define DLLM_PHASE_END(VMWAIT)                                       \
   if (VMWAIT) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");       \
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                 \
+  DLLM_LDS_WAIT();                                                   \
   DLLM_BARRIER();
     // ---- even buffer (tile te) ----
-    read_a(slot(0, 0, 0)); read_b(slot(1, 0, 0), fb0);
+    read_a(I0{}, I0{}); read_b(I0{}, I0{}, fb0);
     stage(0, 1, to, 1);                        // P0: A1 odd
     DLLM_PHASE_END(false)
+    fin_a(); fin_b(fb0);
     mfma_quad(acc[0][0], fb0);
     DLLM_BARRIER();
-    read_b(slot(1, 1, 0), fb1);
+    read_b(I1{}, I0{}, fb1);
     stage(0, 0, te + 2, 0);                    // P1: A0 even
     DLLM_PHASE_END(false)
+    fin_b(fb1);
     mfma_quad(acc[0][1], fb1);
     DLLM_BARRIER();
-    read_a(slot(0, 1, 0));
+    read_a(I1{}, I0{});
     stage(1, 0, te + 2, 0);                    // P2: B0 even
     DLLM_PHASE_END(false)
+    fin_a();
     mfma_quad(acc[1][1], fb1);
     DLLM_BARRIER();
     stage(1, 1, te + 2, 0);                    // P3: B1 even
@@ -498,19 +588,22 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
     mfma_quad(acc[1][0], fb0);
     DLLM_BARRIER();
     // ---- odd buffer (tile to) ----
-    read_a(slot(0, 0, 1)); read_b(slot(1, 0, 1), fb0);
+    read_a(I0{}, I1{}); read_b(I0{}, I1{}, fb0);
     stage(0, 1, te + 2, 0);                    // P4: A1 even
     DLLM_PHASE_END(false)
+    fin_a(); fin_b(fb0);
     mfma_quad(acc[0][0], fb0);
     DLLM_BARRIER();
-    read_b(slot(1, 1, 1), fb1);
+    read_b(I1{}, I1{}, fb1);
     stage(0, 0, to + 2, 1);                    // P5: A0 odd
     DLLM_PHASE_END(false)
+    fin_b(fb1);
     mfma_quad(acc[0][1], fb1);
     DLLM_BARRIER();
-    read_a(slot(0, 1, 1));
+    read_a(I1{}, I1{});
     stage(1, 0, to + 2, 1);                    // P6: B0 odd
     DLLM_PHASE_END(false)
+    fin_a();
     mfma_quad(acc[1][1], fb1);
     DLLM_BARRIER();
     stage(1, 1, to + 2, 1);                    // P7: B1 odd
@@ -903,6 +996,24 @@ int dllm_gemm_set_variant(int v) {
   const int old = g_bf16_variant;
   g_bf16_variant = v;
   return old;
+}
+
+// ablation launcher (performance investigation only): TN layout, bf16 out, square problems
+int dllm_gemm_ablation(int abl, const void* A, const void* B, void* C, int n, void* stream) {
+  GemmArgs a = {};
+  a.A = A; a.B = B; a.C = C; a.lda = n; a.ldb = n; a.ldc = n; a.M = n; a.N = n; a.K = n;
+  a.alpha = 1.f; a.group_m = 4;
+  if (n % 256) return -1;
+  const int nb = (n / 256) * (n / 256);
+  hipStream_t s = (hipStream_t)stream;
+#define DLLM_ABL(X) \
+  case X: hipLaunchKernelGGL((gemm_bf16_8ph<L_TN, EPI_STORE, uint16_t, true, X>), dim3(nb), dim3(512), 0, s, a); break;
+  switch (abl) {
+    DLLM_ABL(0) DLLM_ABL(3) DLLM_ABL(12) DLLM_ABL(15) DLLM_ABL(1) DLLM_ABL(4) DLLM_ABL(5) DLLM_ABL(10)
+    default: return -1;
+  }
+#undef DLLM_ABL
+  return (int)hipGetLastError();
 }
 
 // which kernel family dllm_gemm would pick (for tests / profiling labels)

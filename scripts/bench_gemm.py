@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--group_m", type=int, default=4)
     ap.add_argument("--json", default="")
     ap.add_argument("--variants", default="2stage,8phase,8phase_stagger")
+    ap.add_argument("--cases", default="", help="comma-separated substrings selecting cases")
+    ap.add_argument("--no_torch", action="store_true")
     a = ap.parse_args()
     T, D, F = a.T, a.D, a.F
     bf = torch.bfloat16
@@ -70,7 +72,11 @@ def main():
     flops = 2 * T * D * F
     variants = a.variants.split(",")
     res = {}
+    if a.cases:
+        cases = {k: v for k, v in cases.items() if any(c in k for c in a.cases.split(","))}
     for name, (mine, ref) in cases.items():
+        if a.no_torch:
+            ref = lambda: None  # noqa: E731
         times = {v: [] for v in variants}
         tr = []
         for _ in range(a.rounds):  # interleaved rounds in one process (guide §5.4 rule 24)
