@@ -10,7 +10,9 @@ reference optimizer, train_ffns.py:172), random-init weights and synthetic devic
 
 Each timed step is the full training step: device mock-data generation, forward, backward (all weight
 and input gradients except the unused layer-0 input grad), gradient communication and the optimizer
-update.  K steps are bracketed by cuda synchronize + barrier on both sides; the max over ranks is
+update.  Default parallelism for N>1 is data parallel with ZeRO-2 sharding (bf16 gradient reduce-scatter,
+fp32 master weights sharded 1/N, bf16 weight all-gather); with N=1 there is no gradient collective and
+the SGD update is fused into the weight-gradient GEMM epilogues.  K steps are bracketed by cuda synchronize + barrier on both sides; the max over ranks is
 reported; rank 0 prints ONE JSON line.  Weak scaling: every rank processes 8192 tokens per step under
 DDP/FSDP (global batch = 8·N sequences); ``--method tp`` shards each layer over the GPUs instead
 (tokens per step fixed: strong scaling).
@@ -41,7 +43,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=0)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--method", choices=["ddp", "fsdp", "tp", "hybrid"], default="ddp")
+    p.add_argument("--method", choices=["ddp", "zero", "fsdp", "tp", "hybrid"], default="zero",
+                   help="zero = data parallel with ZeRO-2 (bucketed reduce-scatter overlapped with the backward, "
+                        "1/N sharded optimizer, async all-gather of the bf16 weights overlapped with the next "
+                        "forward); ddp = bucketed all-reduce + full optimizer per rank")
     p.add_argument("--tp", type=int, default=0, help="TP degree for --method hybrid")
     p.add_argument("--model_size", type=int, default=4096)
     p.add_argument("--ffn_dim", type=int, default=0)
@@ -51,7 +56,8 @@ def parse():
     p.add_argument("--act", default="relu")
     p.add_argument("--gated", action="store_true")
     p.add_argument("--dtype", default="bf16")
-    p.add_argument("--grad_dtype", default="fp32")
+    p.add_argument("--grad_dtype", default="bf16",
+                   help="gradient / gradient-collective dtype for N>1 (N=1 fuses the fp32 update into the GEMM)")
     p.add_argument("--optimizer", default="sgd")
     p.add_argument("--bucket_mb", type=float, default=0.0)
     p.add_argument("--recompute", default="none")
@@ -80,6 +86,8 @@ def main() -> int:
 
     if a.method == "ddp":
         dp_mode, dp, tp = "ddp", n, 1
+    elif a.method == "zero":
+        dp_mode, dp, tp = "zero", n, 1
     elif a.method == "fsdp":
         dp_mode, dp, tp = "fsdp", n, 1
     elif a.method == "tp":
@@ -124,7 +132,8 @@ def main() -> int:
     value = tokens_global * a.steps / el
     tflops = flops_per_step(cfg, tp=tp, recompute=cfg.recompute) / (ms / 1e3) / 1e12
     finite = bool(torch.isfinite(eng.master[:1024]).all().item())
-    par = {"ddp": f"dp{n}", "fsdp": f"fsdp{n}", "tp": f"tp{n}", "hybrid": f"fsdp{dp}xtp{tp}"}[a.method]
+    par = {"ddp": f"dp{n}", "zero": f"dp{n}-zero2", "fsdp": f"fsdp{n}", "tp": f"tp{n}",
+           "hybrid": f"fsdp{dp}xtp{tp}"}[a.method]
     rec = {
         "metric": METRIC, "value": round(value, 1), "unit": "tokens/s", "n_gpus": n, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,

@@ -109,8 +109,9 @@ class FFNTrainer:
         multi = d > 1 or cfg.force_comm
         self.fsdp = cfg.dp_mode == "fsdp" and multi
         self.ddp = cfg.dp_mode == "ddp" and multi
+        self.zero = cfg.dp_mode == "zero" and multi
         if d > 1 and cfg.dp_mode == "none":
-            raise ValueError("dp > 1 needs dp_mode ddp or fsdp")
+            raise ValueError("dp > 1 needs dp_mode ddp, zero or fsdp")
         if self.fsdp and (self.R1 % d or D % d):
             raise ValueError(f"FSDP needs W1 rows ({self.R1}) and D ({D}) divisible by dp={d} (train_ffns.py:266)")
         self.cd, self.gd = cfg.torch_dtype, cfg.torch_grad_dtype
@@ -126,12 +127,14 @@ class FFNTrainer:
         full = {"w2": (D, self.F_loc), "w1": (self.R1, D)}
         self.entries: list[Entry] = []
         off = 0
+        # ZeRO shards every bucket evenly over dp ranks: keep every entry a multiple of dp*ALIGN
+        self.align = ALIGN * d if self.zero else ALIGN
         for l in reversed(range(L)):
             for name in ("w2", "w1"):
                 fs = full[name]
                 own = (fs[0] // d, fs[1]) if self.fsdp else fs
                 e = Entry(l, name, own, fs, off)
-                off += _round_up(e.numel, ALIGN)
+                off += _round_up(e.numel, self.align)
                 self.entries.append(e)
         self.total = off
         self.entry = {(e.layer, e.name): e for e in self.entries}
@@ -140,7 +143,7 @@ class FFNTrainer:
         self.copy = self.master if self.shared_copy else torch.zeros(self.total, dtype=self.cd, device=dev)
         # no gradient collective (single device / pure TP): the optimizer runs inside the wgrad GEMMs and
         # no flat gradient buffer exists at all
-        self.fused_opt = cfg.fused_optimizer and not (self.ddp or self.fsdp)
+        self.fused_opt = cfg.fused_optimizer and not (self.ddp or self.fsdp or self.zero)
         self.grads = torch.zeros(0 if self.fused_opt else self.total, dtype=self.gd, device=dev)
         if cfg.optimizer == "adam":
             self.adam_m = torch.zeros(self.total, dtype=torch.float32, device=dev)
@@ -175,17 +178,34 @@ class FFNTrainer:
             self.dyfull = torch.empty((T, D), dtype=self.cd, device=dev)
             self.dxs = [torch.empty((Tl, D), dtype=self.cd, device=dev) for _ in range(2)]
 
-        # ---- DDP buckets -------------------------------------------------------------------------
+        # ---- DDP / ZeRO buckets ------------------------------------------------------------------
         self.buckets = []  # (start, end, last_entry_index)
-        if self.ddp:
+        if self.ddp or self.zero:
             cap = int(cfg.bucket_mb * 2**20 / self.grads.element_size()) if cfg.bucket_mb > 0 else 0
             start = 0
             for i, e in enumerate(self.entries):
-                end = e.offset + _round_up(e.numel, ALIGN)
+                end = e.offset + _round_up(e.numel, self.align)
                 if cap == 0 or end - start >= cap or i == len(self.entries) - 1:
                     self.buckets.append((start, end, i))
                     start = end
             self.bucket_work = [None] * len(self.buckets)
+        if self.zero:
+            # rank r owns [s + r*(e-s)/d, s + (r+1)*(e-s)/d) of every bucket
+            self.gshard = torch.zeros(self.total // d, dtype=self.gd, device=dev)
+            self.bucket_shard = []
+            goff = 0
+            for s_, e_, _ in self.buckets:
+                n = (e_ - s_) // d
+                self.bucket_shard.append((s_ + mesh.dp_rank * n, s_ + (mesh.dp_rank + 1) * n, goff))
+                goff += n
+            self.ag_pending = [None] * len(self.buckets)
+            self.rs_issued_at = [None] * len(self.buckets)
+            self.layer_buckets = {l: sorted({b for b, (s_, e_, _) in enumerate(self.buckets)
+                                             for n in ("w1", "w2")
+                                             if s_ < self.entry[(l, n)].offset + self.entry[(l, n)].numel
+                                             and self.entry[(l, n)].offset < e_})
+                                  for l in range(L)}
+            self._master_synced = True
         self._entry_index = {(e.layer, e.name): i for i, e in enumerate(self.entries)}
         self._next_bucket = 0
 
@@ -206,7 +226,7 @@ class FFNTrainer:
 
     def _layer_range(self, l: int) -> tuple[int, int]:
         e2, e1 = self.entry[(l, "w2")], self.entry[(l, "w1")]
-        return e2.offset, e1.offset + _round_up(e1.numel, ALIGN)
+        return e2.offset, e1.offset + _round_up(e1.numel, self.align)
 
     # ------------------------------------------------------------------------------------------------
     # parameters in / out (logical layout: per layer w1 [F,D], w2 [D,F] (+ w3 [F,D] if gated))
@@ -221,7 +241,10 @@ class FFNTrainer:
         return {"w1": w1, "w2": w2}
 
     def flat_buffers(self) -> dict:
-        """Named flat fp32 state buffers sharing the parameter layout (checkpointed)."""
+        """Named flat fp32 state buffers sharing the parameter layout (checkpointed).  Under ZeRO the
+        owned shards are all-gathered first so every buffer is complete on every rank (collective)."""
+        if self.zero:
+            self.zero_sync_state()
         out = {"params": self.master}
         if self.cfg.optimizer == "adam":
             out["adam_m"], out["adam_v"] = self.adam_m, self.adam_v
@@ -247,6 +270,21 @@ class FFNTrainer:
             cast_(self.master, self.copy)
 
     @torch.no_grad()
+    def zero_sync_state(self) -> None:
+        """ZeRO: finish in-flight parameter all-gathers and all-gather the fp32 master (and Adam moment)
+        shards so the flat buffers hold full values on every rank (checkpoint / gather).  Collective."""
+        if not self.zero:
+            return
+        for b in range(len(self.buckets)):
+            self._zero_wait_ag(b)
+        bufs = [self.master] + ([self.adam_m, self.adam_v] if self.cfg.optimizer == "adam" else [])
+        grp = self.mesh.group("dp_ag")
+        for buf in bufs:
+            for b, (s_, e_, _) in enumerate(self.buckets):
+                ss, se, _ = self.bucket_shard[b]
+                comm.all_gather_into(buf[s_:e_], buf[ss:se].clone(), grp, async_op=False)
+
+    @torch.no_grad()
     def local_params(self, flat: torch.Tensor | None = None) -> list[dict]:
         """This TP rank's full local (unsharded over dp) fp32 tensors of a flat buffer, w1 de-interleaved.
         Collective over the dp group under FSDP."""
@@ -270,6 +308,8 @@ class FFNTrainer:
     @torch.no_grad()
     def gather_full_params(self, flat: torch.Tensor | None = None) -> list[dict] | None:
         """Full logical fp32 tensors on CPU at global rank 0 (None elsewhere).  Collective."""
+        if self.zero and flat is None:
+            self.zero_sync_state()
         loc = self.local_params(flat)
         res = []
         for p in loc:
@@ -308,7 +348,17 @@ class FFNTrainer:
     # communication hooks
     # ------------------------------------------------------------------------------------------------
     def _grad_ready(self, l: int, name: str) -> None:
-        if self.ddp:
+        if self.zero:
+            idx = self._entry_index[(l, name)]
+            while self._next_bucket < len(self.buckets) and self.buckets[self._next_bucket][2] <= idx:
+                b = self._next_bucket
+                s_, e_, _ = self.buckets[b]
+                ss, se, go = self.bucket_shard[b]
+                self.bucket_work[b] = comm.reduce_scatter_into(self.gshard[go:go + (se - ss)], self.grads[s_:e_],
+                                                               self.mesh.group("dp_rs"), async_op=True)
+                self.rs_issued_at[b] = l
+                self._next_bucket += 1
+        elif self.ddp:
             idx = self._entry_index[(l, name)]
             while self._next_bucket < len(self.buckets) and self.buckets[self._next_bucket][2] <= idx:
                 b = self._next_bucket
@@ -321,6 +371,31 @@ class FFNTrainer:
             works = [comm.reduce_scatter_into(self.grad_view(l, n), g[n], self.mesh.group("dp_rs"), async_op=True)
                      for n in ("w2", "w1")]
             self.rs_pending[slot] = (l, works)
+
+    def _zero_finish(self, b: int) -> None:
+        """Bucket b's reduce-scatter is done -> update the owned shard -> all-gather the new bf16 copy."""
+        self.bucket_work[b].wait()
+        self.bucket_work[b] = None
+        s_, e_, _ = self.buckets[b]
+        ss, se, go = self.bucket_shard[b]
+        cfg = self.cfg
+        g = self.gshard[go:go + (se - ss)]
+        copy = None if self.shared_copy else self.copy[ss:se]
+        if cfg.optimizer == "sgd":
+            sgd_step_(self.master[ss:se], g, cfg.lr, copy=copy)
+        else:
+            adam_step_(self.master[ss:se], g, self.adam_m[ss:se], self.adam_v[ss:se], self.step_count, cfg.lr,
+                       cfg.adam_b1, cfg.adam_b2, cfg.adam_eps, cfg.weight_decay, copy=copy)
+        src = self.copy[ss:se]
+        if self.device.type != "cuda":
+            src = src.clone()  # gloo: keep input and output of the all-gather disjoint
+        self.ag_pending[b] = comm.all_gather_into(self.copy[s_:e_], src, self.mesh.group("dp_ag"), async_op=True)
+        self.rs_issued_at[b] = None
+
+    def _zero_wait_ag(self, b: int) -> None:
+        if self.ag_pending[b] is not None:
+            self.ag_pending[b].wait()
+            self.ag_pending[b] = None
 
     def _fsdp_finish_rs(self, slot: int) -> None:
         pend = self.rs_pending[slot]
@@ -379,6 +454,9 @@ class FFNTrainer:
                 if l + 1 < L:
                     self._fsdp_gather(l + 1)
             else:
+                if self.zero:
+                    for b in self.layer_buckets[l]:
+                        self._zero_wait_ag(b)
                 w1, w2 = self.copy_view(l, "w1"), self.copy_view(l, "w2")
             a = self.acts_a[l if keep else 0]
             h = (self.acts_h[l if keep else 0]) if self.need_h else None
@@ -446,9 +524,19 @@ class FFNTrainer:
                                self.dxb[l % 2] if need_dx else None, hooks)
                 if dx is not None:
                     g = dx
+            if self.zero:
+                # reduce-scatters issued during an earlier layer have had a full layer of compute to
+                # finish: update those shards now (1/dp of the optimizer work, off the tail)
+                for b, at in enumerate(self.rs_issued_at):
+                    if at is not None and at > l:
+                        self._zero_finish(b)
 
         # ---------------- optimizer ----------------
-        if self.ddp:
+        if self.zero:
+            for b, at in enumerate(self.rs_issued_at):
+                if at is not None:
+                    self._zero_finish(b)
+        elif self.ddp:
             for b, (s, e, _) in enumerate(self.buckets):
                 self.bucket_work[b].wait()
                 self._opt(s, e)

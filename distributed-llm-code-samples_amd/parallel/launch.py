@@ -31,6 +31,7 @@ METHOD_MESH = {  # method -> (dp_mode, dp, tp) given n ranks
     3: lambda n, a: ("fsdp", n, 1),
     4: lambda n, a: ("none", 1, n),
     5: lambda n, a: (a.get("hybrid_dp_mode", "fsdp"), n // a["tp"], a["tp"]),
+    6: lambda n, a: ("zero", n, 1),
 }
 
 

@@ -3,7 +3,8 @@
     python train_ffns.py --num_steps 16 --batch_size 8 --seq_len 1024 --layers 1 --model_size 8192 --method M
 
 ``M``: 0 = all methods, 1 = single GPU, 2 = DDP, 3 = FSDP (ZeRO-3 + DP), 4 = TP ("MP", Megatron),
-5 = hybrid (FSDP or DDP) × TP.  Reference flags keep their names and defaults; the extended flags
+5 = hybrid (FSDP / ZeRO / DDP) × TP, 6 = ZeRO-2 data parallel (reduce-scatter, sharded optimizer,
+all-gather).  Reference flags keep their names and defaults; the extended flags
 (``--dtype bf16 --act silu --gated --optimizer adam --ffn_dim …``) add the north-star features.
 
 Stdout keeps the reference's lines (``ARGS:`` block, ``PARAMS:``, initial/final ``[:5,:5]`` slices,
@@ -25,7 +26,7 @@ from .parallel.launch import build_params, spawn
 from .utils.config import METHODS, ModelConfig, TrainConfig, add_extended_args, add_reference_args
 from .utils.metrics import jsonl
 
-FN_NAMES = {1: "train_1gpu", 2: "train_ddp", 3: "train_fsdp", 4: "train_tp", 5: "train_hybrid"}
+FN_NAMES = {1: "train_1gpu", 2: "train_ddp", 3: "train_fsdp", 4: "train_tp", 5: "train_hybrid", 6: "train_zero"}
 
 
 def make_parser() -> argparse.ArgumentParser:

@@ -15,7 +15,7 @@ LR = 1e-5            # train_ffns.py:29
 DLOSS_DX_COEF = 0.1  # train_ffns.py:30
 INIT_SCALE = 2e-2    # train_ffns.py:35
 SEED_RANGE = 100_000  # train_ffns.py:360
-METHODS = {0: "all", 1: "1gpu", 2: "ddp", 3: "fsdp", 4: "tp", 5: "hybrid"}
+METHODS = {0: "all", 1: "1gpu", 2: "ddp", 3: "fsdp", 4: "tp", 5: "hybrid", 6: "zero"}
 
 
 @dataclass
@@ -54,7 +54,7 @@ class TrainConfig:
     adam_b2: float = 0.95
     adam_eps: float = 1e-8
     weight_decay: float = 0.0
-    dp_mode: str = "none"            # none | ddp | fsdp
+    dp_mode: str = "none"            # none | ddp | zero (ZeRO-2: sharded optimizer) | fsdp (ZeRO-3)
     dp: int = 1
     tp: int = 1
     sequence_parallel: bool = False  # Megatron SP for the TP path (RS/AG over T instead of AR)
@@ -87,7 +87,8 @@ def add_reference_args(p: argparse.ArgumentParser) -> None:
     p.add_argument("-l", "--layers", type=int, default=1)
     p.add_argument("-d", "--model_size", type=int, default=4)
     p.add_argument("-m", "--method", type=int, default=0,
-                   help="0=all, 1=1gpu, 2=DDP, 3=FSDP, 4=TP (MP), 5=hybrid FSDP/DDP x TP")
+                   help="0=all, 1=1gpu, 2=DDP, 3=FSDP, 4=TP (MP), 5=hybrid FSDP/DDP x TP, "
+                        "6=ZeRO-2 data parallel (sharded optimizer)")
     p.add_argument("-r", "--random_seed", type=int, default=0)
 
 
@@ -104,7 +105,7 @@ def add_extended_args(p: argparse.ArgumentParser) -> None:
     p.add_argument("--nprocs", type=int, default=0, help="ranks to spawn (0 = all visible GPUs)")
     p.add_argument("--dp", type=int, default=0)
     p.add_argument("--tp", type=int, default=0)
-    p.add_argument("--hybrid_dp_mode", choices=["ddp", "fsdp"], default="fsdp")
+    p.add_argument("--hybrid_dp_mode", choices=["ddp", "zero", "fsdp"], default="fsdp")
     p.add_argument("--sequence_parallel", action="store_true")
     p.add_argument("--recompute", choices=["none", "full"], default="none")
     p.add_argument("--bucket_mb", type=float, default=0.0)

@@ -133,3 +133,25 @@ def test_worker_failure_propagates(free_port):
     cfg = _cfg(D=30, L=1)  # FSDP over 4 ranks: D=30 not divisible -> every rank raises
     with pytest.raises(RuntimeError, match="divisible"):
         spawn(4, cfg, 3, "gloo", free_port, {"seed": 1, "init": "cpu_compat"})
+
+
+@pytest.mark.parametrize("opt,bucket", [("sgd", 0.0), ("sgd", 0.01), ("adam", 0.0)])
+def test_zero2_equals_ddp(opt, bucket, free_port):
+    cfg = _cfg(L=3, steps=4, optimizer=opt, lr=1e-3 if opt == "adam" else 1e-2, bucket_mb=bucket)
+    ddp = _run(cfg, 2, 2, free_port)
+    zero = _run(cfg, 6, 2, free_port + 1)
+    _close(zero, ddp, rtol=1e-6, atol=1e-8)
+
+
+def test_zero2_world4_and_hybrid(free_port):
+    cfg = _cfg(L=2, steps=4)
+    _close(_run(cfg, 6, 4, free_port), _oracle(cfg, 4))
+    _close(_run(cfg, 5, 4, free_port + 1, tp=2, hybrid_dp_mode="zero"), _oracle(cfg, 2))
+
+
+def test_zero2_checkpoint_resume(tmp_path, free_port):
+    cfg = _cfg(L=2, steps=4, optimizer="adam", lr=1e-3)
+    full = _run(cfg, 6, 2, free_port)
+    ck = str(tmp_path / "z")
+    _run(cfg, 6, 2, free_port + 1, ckpt_dir=ck, stop_after=1, ckpt_format="sharded")
+    _close(_run(cfg, 6, 2, free_port + 2, resume=ck), full, rtol=1e-6, atol=1e-8)
