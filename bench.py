@@ -64,6 +64,8 @@ def parse():
     p.add_argument("--sequence_parallel", action="store_true")
     p.add_argument("--seed", type=int, default=1234)
     p.add_argument("--json_out", default="")
+    p.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                   help="gloo = CPU dry run of the multi-rank path (tests; tiny dims)")
     p.add_argument("--force_comm", action="store_true",
                    help="exercise the RCCL DDP/FSDP path at N=1 (size-1 communicators, unfused optimizer)")
     return p.parse_args()
@@ -76,13 +78,15 @@ def main() -> int:
     n = a.gpus or world
     if n != world:
         raise SystemExit(f"--gpus {n} but WORLD_SIZE={world}: launch N>1 with torchrun")
+    cpu = a.backend == "gloo"
     if world > 1 or a.force_comm:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
-        init_distributed("nccl")
-    else:
+        init_distributed(a.backend)
+    elif not cpu:
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
-    dev = torch.device("cuda", torch.cuda.current_device())
+    dev = torch.device("cpu") if cpu else torch.device("cuda", torch.cuda.current_device())
+    sync = (lambda: None) if cpu else torch.cuda.synchronize
 
     if a.method == "ddp":
         dp_mode, dp, tp = "ddp", n, 1
@@ -105,20 +109,20 @@ def main() -> int:
     from dllm.models.ffn import init_ffn_params_device
 
     eng.load_full_params(init_ffn_params_device(m.D, m.F, m.layers, a.seed, dev, m.gated))
-    torch.cuda.synchronize()
+    sync()
     data = DeviceMockData(cfg.tokens, m.D, cfg.torch_dtype, dev)
     seed_base = 10_000 * (mesh.dp_rank + 1)
 
     for i in range(a.warmup):
         x, dy = data.fill(seed_base + i)
         eng.train_step(x, dy)
-    torch.cuda.synchronize()
+    sync()
     comm.barrier(device=dev)
     t0 = time.perf_counter()
     for i in range(a.steps):
         x, dy = data.fill(seed_base + a.warmup + i)
         eng.train_step(x, dy)
-    torch.cuda.synchronize()
+    sync()
     comm.barrier(device=dev)
     el = time.perf_counter() - t0
     if world > 1:
@@ -132,10 +136,12 @@ def main() -> int:
     value = tokens_global * a.steps / el
     tflops = flops_per_step(cfg, tp=tp, recompute=cfg.recompute) / (ms / 1e3) / 1e12
     finite = bool(torch.isfinite(eng.master[:1024]).all().item())
+    if eng.zero:
+        eng.zero_sync_state()  # quiesce in-flight weight all-gathers before teardown
     par = {"ddp": f"dp{n}", "zero": f"dp{n}-zero2", "fsdp": f"fsdp{n}", "tp": f"tp{n}",
            "hybrid": f"fsdp{dp}xtp{tp}"}[a.method]
     rec = {
-        "metric": METRIC, "value": round(value, 1), "unit": "tokens/s", "n_gpus": n, "steps": a.steps,
+        "metric": METRIC, "value": round(value, 1), "unit": "tokens/s", "n_gpus": 0 if cpu else n, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
         "scaling": "strong" if a.method == "tp" else "weak", "vs_baseline": None, "dtype": a.dtype,
         "data": "synthetic (device Philox N(0,1) x, 0.1*N(0,1) dloss/dx; random-init weights)",
@@ -146,6 +152,8 @@ def main() -> int:
     }
     if a.force_comm:
         rec["note"] = "force_comm: DDP/FSDP collectives over size-1 RCCL communicators"
+    if cpu:
+        rec["note"] = f"CPU/gloo dry run with {world} ranks (plumbing only, not a measurement)"
     if rank == 0:
         print(json.dumps(rec), flush=True)
         if a.json_out:
