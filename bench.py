@@ -64,6 +64,8 @@ def parse():
     p.add_argument("--sequence_parallel", action="store_true")
     p.add_argument("--seed", type=int, default=1234)
     p.add_argument("--json_out", default="")
+    p.add_argument("--comm", choices=["torch", "native"], default="torch",
+                   help="role communicators: torch ProcessGroupNCCL or the native C++ RCCL layer")
     p.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                    help="gloo = CPU dry run of the multi-rank path (tests; tiny dims)")
     p.add_argument("--force_comm", action="store_true",
@@ -103,8 +105,9 @@ def main() -> int:
     cfg = TrainConfig(model=m, batch_size=a.batch_size, seq_len=a.seq_len, num_steps=a.steps, dtype=a.dtype,
                       grad_dtype=a.grad_dtype, optimizer=a.optimizer, dp_mode=dp_mode, dp=dp, tp=tp,
                       bucket_mb=a.bucket_mb, recompute=a.recompute, sequence_parallel=a.sequence_parallel,
-                      data="device", force_comm=a.force_comm)
-    mesh = Mesh.build(dp, tp, force=a.force_comm)
+                      data="device", force_comm=a.force_comm, comm_backend=a.comm)
+    mesh = Mesh.build(dp, tp, force=a.force_comm, comm_backend="torch" if cpu else a.comm,
+                      device=None if cpu else dev)
     eng = FFNTrainer(cfg, mesh, dev)
     from dllm.models.ffn import init_ffn_params_device
 
@@ -148,7 +151,7 @@ def main() -> int:
         "config": {"model": f"ffn-stack L{m.layers} D{m.D} F{m.F} {'swiglu-' if m.gated else ''}{m.act}",
                    "global_batch": a.batch_size * dp, "seq_len": a.seq_len, "parallelism": par,
                    "optimizer": a.optimizer, "grad_dtype": a.grad_dtype, "master_weights": "fp32"},
-        "tflops_per_gpu": round(tflops, 1), "finite": finite,
+        "tflops_per_gpu": round(tflops, 1), "finite": finite, "comm": a.comm,
     }
     if a.force_comm:
         rec["note"] = "force_comm: DDP/FSDP collectives over size-1 RCCL communicators"
@@ -162,6 +165,8 @@ def main() -> int:
     import torch.distributed as dist
 
     if dist.is_initialized():
+        dist.barrier()
+        mesh.destroy()
         dist.destroy_process_group()
     return 0
 

@@ -30,6 +30,12 @@ class Done:
         return True
 
 
+def _native(group) -> bool:
+    from .rccl import NativeGroup
+
+    return isinstance(group, NativeGroup)
+
+
 def _active(group) -> bool:
     """A collective on ``None`` (a mesh axis of size 1 without a communicator) is a local no-op; a real
     group — even of size 1 (``Mesh.build(force=True)``) — always goes through the backend."""
@@ -37,6 +43,9 @@ def _active(group) -> bool:
 
 
 def all_reduce(t: torch.Tensor, group, async_op: bool = True):
+    if group is not None and _native(group):
+        w = group.all_reduce(t)
+        return w if async_op else (w.wait(), Done())[1]
     if not _active(group):
         return Done()
     w = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
@@ -44,6 +53,9 @@ def all_reduce(t: torch.Tensor, group, async_op: bool = True):
 
 
 def all_gather_into(out: torch.Tensor, shard: torch.Tensor, group, async_op: bool = True):
+    if group is not None and _native(group):
+        w = group.all_gather_into(out.view(-1), shard.reshape(-1))
+        return w if async_op else (w.wait(), Done())[1]
     if not _active(group):
         if out.data_ptr() != shard.data_ptr():
             out.copy_(shard.view_as(out))
@@ -56,6 +68,9 @@ def all_gather_into(out: torch.Tensor, shard: torch.Tensor, group, async_op: boo
 
 
 def reduce_scatter_into(out: torch.Tensor, full: torch.Tensor, group, async_op: bool = True):
+    if group is not None and _native(group):
+        w = group.reduce_scatter_into(out.view(-1), full.reshape(-1))
+        return w if async_op else (w.wait(), Done())[1]
     if not _active(group):
         if out.data_ptr() != full.data_ptr():
             out.copy_(full.view_as(out))
@@ -70,6 +85,11 @@ def reduce_scatter_into(out: torch.Tensor, full: torch.Tensor, group, async_op: 
 
 def gather_to_rank0(t: torch.Tensor, group=None) -> list[torch.Tensor] | None:
     """Gather equally-shaped tensors from every rank of ``group`` onto rank 0 of that group (CPU copies)."""
+    if group is not None and _native(group):
+        n = group.size()
+        out = torch.empty((n,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        group.all_gather_into(out.view(-1), t.contiguous().view(-1)).wait()
+        return [o.cpu() for o in out]
     if group is None or not dist.is_initialized() or dist.get_world_size(group) == 1:
         return [t.detach().cpu()]
     n = dist.get_world_size(group)

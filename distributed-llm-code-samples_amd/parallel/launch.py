@@ -75,7 +75,8 @@ def run_rank(rank: int, world: int, cfg_dict: dict, method: int, backend: str, p
         device = torch.device("cuda", torch.cuda.current_device())
     dp_mode, dp, tp = METHOD_MESH[method](world, opts)
     cfg.dp_mode, cfg.dp, cfg.tp = dp_mode, dp, tp
-    mesh = Mesh.build(dp, tp, separate_streams=cfg.separate_streams)
+    mesh = Mesh.build(dp, tp, separate_streams=cfg.separate_streams, comm_backend=cfg.comm_backend,
+                      device=device if device.type == "cuda" else None)
     eng = FFNTrainer(cfg, mesh, device)
 
     seed = int(opts["seed"])
@@ -122,6 +123,7 @@ def run_rank(rank: int, world: int, cfg_dict: dict, method: int, backend: str, p
         import torch.distributed as dist
 
         dist.barrier()
+        mesh.destroy()
         dist.destroy_process_group()
     if queue is not None and rank == 0:
         queue.put(("ok", to_numpy(rec)))  # by-value payload: survives the worker's exit

@@ -10,7 +10,9 @@ or ``gloo`` (CPU plumbing), and a ``Mesh`` of ``dp × tp`` ranks (tp fastest-var
 block of neighbouring GPUs).  Each communication *role* gets its own process group — and therefore its
 own RCCL communicator and HIP stream — so DDP gradient all-reduce, FSDP parameter all-gather, FSDP
 gradient reduce-scatter and TP activation all-reduce can run concurrently with each other and with
-compute:
+compute.  Two interchangeable communicator implementations: torch ProcessGroupNCCL (``comm_backend=
+"torch"``, default) or the native C++ RCCL layer (``"native"``: ``csrc/comm.cpp`` + ``parallel/rccl.py``,
+one ncclComm_t + one hipStream_t per role, store-bootstrapped, event-synchronised):
 
     role      ranks        used by
     dp_ar     dp group     DDP bucketed gradient all-reduce
@@ -76,8 +78,20 @@ class Mesh:
     def group(self, role: str):
         return self.groups.get(role)
 
+    def destroy(self) -> None:
+        """Tear down native communicators (torch process groups are destroyed with the default PG)."""
+        from .rccl import NativeGroup
+
+        seen = set()
+        for g in self.groups.values():
+            if isinstance(g, NativeGroup) and id(g) not in seen:
+                seen.add(id(g))
+                g.destroy()
+        self.groups.clear()
+
     @classmethod
-    def build(cls, dp: int, tp: int, separate_streams: bool = True, force: bool = False) -> "Mesh":
+    def build(cls, dp: int, tp: int, separate_streams: bool = True, force: bool = False,
+              comm_backend: str = "torch", device: torch.device | None = None) -> "Mesh":
         """Create the role process groups (collective: every rank must call it with the same args).
 
         ``force`` also creates groups for axes of size 1 (used to exercise the RCCL code paths with a
@@ -90,6 +104,20 @@ class Mesh:
         m.dp_ranks = [d * tp + m.tp_rank for d in range(dp)]
         m.tp_ranks = [m.dp_rank * tp + t for t in range(tp)]
         if not dist.is_initialized() or (world == 1 and not force):
+            return m
+        if comm_backend == "native":
+            from .rccl import new_role_group
+
+            dev = device or torch.device("cuda", torch.cuda.current_device())
+            for role in ROLES:
+                axis = dp if role.startswith("dp") else tp
+                if axis == 1 and not force:
+                    continue
+                if not separate_streams and role in ("dp_ag", "dp_rs") and "dp_ar" in m.groups:
+                    m.groups[role] = m.groups["dp_ar"]
+                    continue
+                ranks = m.tp_ranks if role == "tp" else m.dp_ranks
+                m.groups[role] = new_role_group(ranks, role, dev)
             return m
         # every rank creates every group in the same order (new_group is collective)
         for role in ROLES:

@@ -66,6 +66,7 @@ class TrainConfig:
     tp_overlap: bool = True          # overlap the TP dx all-reduce with the dW1 GEMM
     fused_optimizer: bool = True     # fuse SGD/Adam into the wgrad GEMM epilogue when no grad collective
     force_comm: bool = False         # run the DDP/FSDP collective path even at dp=1 (single-GPU RCCL check)
+    comm_backend: str = "torch"      # torch (ProcessGroupNCCL/gloo) | native (csrc/comm.cpp RCCL layer)
 
     @property
     def tokens(self) -> int:
@@ -102,6 +103,8 @@ def add_extended_args(p: argparse.ArgumentParser) -> None:
     p.add_argument("--lr", type=float, default=LR)
     p.add_argument("--weight_decay", type=float, default=0.0)
     p.add_argument("--backend", choices=["auto", "nccl", "rccl", "gloo"], default="auto")
+    p.add_argument("--comm", choices=["torch", "native"], default="torch",
+                   help="communicator implementation for the role groups (native = C++ RCCL layer)")
     p.add_argument("--nprocs", type=int, default=0, help="ranks to spawn (0 = all visible GPUs)")
     p.add_argument("--dp", type=int, default=0)
     p.add_argument("--tp", type=int, default=0)
