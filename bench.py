@@ -68,6 +68,8 @@ def parse():
                    help="role communicators: torch ProcessGroupNCCL or the native C++ RCCL layer")
     p.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                    help="gloo = CPU dry run of the multi-rank path (tests; tiny dims)")
+    p.add_argument("--graph", action="store_true",
+                   help="capture the whole step (data + fwd + bwd + fused SGD) in a HIP graph (N=1 path)")
     p.add_argument("--force_comm", action="store_true",
                    help="exercise the RCCL DDP/FSDP path at N=1 (size-1 communicators, unfused optimizer)")
     return p.parse_args()
@@ -116,15 +118,26 @@ def main() -> int:
     data = DeviceMockData(cfg.tokens, m.D, cfg.torch_dtype, dev)
     seed_base = 10_000 * (mesh.dp_rank + 1)
 
+    graphed = None
+    if a.graph:
+        from dllm.utils.graphs import GraphedStep
+
+        graphed = GraphedStep(eng, cfg.tokens, m.D)
+
+    def one_step(seed):
+        if graphed is not None:
+            graphed.step(seed)
+        else:
+            x, dy = data.fill(seed)
+            eng.train_step(x, dy)
+
     for i in range(a.warmup):
-        x, dy = data.fill(seed_base + i)
-        eng.train_step(x, dy)
+        one_step(seed_base + i)
     sync()
     comm.barrier(device=dev)
     t0 = time.perf_counter()
     for i in range(a.steps):
-        x, dy = data.fill(seed_base + a.warmup + i)
-        eng.train_step(x, dy)
+        one_step(seed_base + a.warmup + i)
     sync()
     comm.barrier(device=dev)
     el = time.perf_counter() - t0
@@ -151,7 +164,7 @@ def main() -> int:
         "config": {"model": f"ffn-stack L{m.layers} D{m.D} F{m.F} {'swiglu-' if m.gated else ''}{m.act}",
                    "global_batch": a.batch_size * dp, "seq_len": a.seq_len, "parallelism": par,
                    "optimizer": a.optimizer, "grad_dtype": a.grad_dtype, "master_weights": "fp32"},
-        "tflops_per_gpu": round(tflops, 1), "finite": finite, "comm": a.comm,
+        "tflops_per_gpu": round(tflops, 1), "finite": finite, "comm": a.comm, "hip_graph": bool(a.graph),
     }
     if a.force_comm:
         rec["note"] = "force_comm: DDP/FSDP collectives over size-1 RCCL communicators"

@@ -38,7 +38,9 @@ __device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, float& z0, fl
 
 template <typename OutT>
 __global__ __launch_bounds__(256) void rng_normal_kernel(OutT* out, long n, uint64_t seed, uint64_t offset,
-                                                         float scale) {
+                                                         float scale, const unsigned long long* seed_dev) {
+  // seed_dev (nullable): read the key from device memory so a captured graph can replay with new seeds
+  if (seed_dev) seed = *seed_dev;
   const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
   const long n4 = (n + 3) / 4;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
@@ -142,17 +144,28 @@ using namespace dllm;
 
 extern "C" {
 
-int dllm_rng_normal(void* out, int dtype, long n, unsigned long long seed, unsigned long long offset, float scale,
-                    void* stream) {
+static int rng_launch(void* out, int dtype, long n, unsigned long long seed, unsigned long long offset, float scale,
+                      const unsigned long long* seed_dev, void* stream) {
   if (n <= 0) return 0;
   const int g = grid_for((n + 3) / 4);
   if (dtype == DT_BF16)
     hipLaunchKernelGGL(rng_normal_kernel<uint16_t>, dim3(g), dim3(256), 0, (hipStream_t)stream, (uint16_t*)out, n,
-                       (uint64_t)seed, (uint64_t)offset, scale);
+                       (uint64_t)seed, (uint64_t)offset, scale, seed_dev);
   else
     hipLaunchKernelGGL(rng_normal_kernel<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, (float*)out, n,
-                       (uint64_t)seed, (uint64_t)offset, scale);
+                       (uint64_t)seed, (uint64_t)offset, scale, seed_dev);
   return (int)hipGetLastError();
+}
+
+int dllm_rng_normal(void* out, int dtype, long n, unsigned long long seed, unsigned long long offset, float scale,
+                    void* stream) {
+  return rng_launch(out, dtype, n, seed, offset, scale, nullptr, stream);
+}
+
+// graph-capturable variant: the seed is read from device memory at execution time
+int dllm_rng_normal_devseed(void* out, int dtype, long n, const unsigned long long* seed_dev,
+                            unsigned long long offset, float scale, void* stream) {
+  return rng_launch(out, dtype, n, 0, offset, scale, seed_dev, stream);
 }
 
 int dllm_sgd_step(float* master, const void* grad, int grad_dtype, void* copy_bf16, long n, float lr, float gscale,

@@ -29,6 +29,21 @@ def rng_normal_(out: torch.Tensor, seed: int, stream_id: int = 0, scale: float =
     return out
 
 
+def rng_normal_devseed_(out: torch.Tensor, seed_dev: torch.Tensor, stream_id: int = 0,
+                        scale: float = 1.0) -> torch.Tensor:
+    """``rng_normal_`` with the seed read from a 1-element int64 device tensor at execution time, so the
+    launch can live inside a captured HIP graph and still draw new data on every replay."""
+    if out.device.type != "cuda":
+        return rng_normal_(out, int(seed_dev.item()), stream_id, scale)
+    if seed_dev.dtype != torch.int64 or seed_dev.device != out.device:
+        raise TypeError("seed_dev must be an int64 tensor on the output's device")
+    rc = _native.lib().dllm_rng_normal_devseed(out.data_ptr(), _native.dtype_code(out.dtype), out.numel(),
+                                               seed_dev.data_ptr(), stream_id & (2**64 - 1), float(scale),
+                                               _native.stream_ptr(out.device))
+    _native.check(rc, "dllm_rng_normal_devseed")
+    return out
+
+
 def _mulhilo(a: int, b: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
     p = b.to(torch.int64) * a  # < 2^64, fits as unsigned; use int64 with masking
     lo = p & 0xFFFFFFFF

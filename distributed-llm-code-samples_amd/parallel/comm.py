@@ -30,6 +30,26 @@ class Done:
         return True
 
 
+_SERIALIZE = False
+
+
+def set_serialize(flag: bool) -> None:
+    """Race-detection mode: every collective is waited for at issue and the device is
+    synchronised, so communication never overlaps compute.  Results must be bitwise identical to the
+    overlapped schedule; any difference exposes a missing stream/event edge."""
+    global _SERIALIZE
+    _SERIALIZE = flag
+
+
+def _finish(w, async_op: bool):
+    if _SERIALIZE and not isinstance(w, Done):
+        w.wait()
+        if torch.cuda.is_available() and torch.cuda.is_initialized():
+            torch.cuda.synchronize()
+        return Done()
+    return w if async_op else Done()
+
+
 def _native(group) -> bool:
     from .rccl import NativeGroup
 
@@ -45,17 +65,17 @@ def _active(group) -> bool:
 def all_reduce(t: torch.Tensor, group, async_op: bool = True):
     if group is not None and _native(group):
         w = group.all_reduce(t)
-        return w if async_op else (w.wait(), Done())[1]
+        return _finish(w, async_op) if (async_op or _SERIALIZE) else (w.wait(), Done())[1]
     if not _active(group):
         return Done()
-    w = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
-    return w if async_op else Done()
+    w = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=True)
+    return _finish(w, async_op) if (async_op or _SERIALIZE) else (w.wait(), Done())[1]
 
 
 def all_gather_into(out: torch.Tensor, shard: torch.Tensor, group, async_op: bool = True):
     if group is not None and _native(group):
         w = group.all_gather_into(out.view(-1), shard.reshape(-1))
-        return w if async_op else (w.wait(), Done())[1]
+        return _finish(w, async_op) if (async_op or _SERIALIZE) else (w.wait(), Done())[1]
     if not _active(group):
         if out.data_ptr() != shard.data_ptr():
             out.copy_(shard.view_as(out))
@@ -63,14 +83,14 @@ def all_gather_into(out: torch.Tensor, shard: torch.Tensor, group, async_op: boo
     n = dist.get_world_size(group)
     if out.numel() != shard.numel() * n:
         raise ValueError(f"all_gather_into: out {out.numel()} != {n} x shard {shard.numel()}")
-    w = dist.all_gather_into_tensor(out.view(-1), shard.reshape(-1), group=group, async_op=async_op)
-    return w if async_op else Done()
+    w = dist.all_gather_into_tensor(out.view(-1), shard.reshape(-1), group=group, async_op=True)
+    return _finish(w, async_op) if (async_op or _SERIALIZE) else (w.wait(), Done())[1]
 
 
 def reduce_scatter_into(out: torch.Tensor, full: torch.Tensor, group, async_op: bool = True):
     if group is not None and _native(group):
         w = group.reduce_scatter_into(out.view(-1), full.reshape(-1))
-        return w if async_op else (w.wait(), Done())[1]
+        return _finish(w, async_op) if (async_op or _SERIALIZE) else (w.wait(), Done())[1]
     if not _active(group):
         if out.data_ptr() != full.data_ptr():
             out.copy_(full.view_as(out))
@@ -79,8 +99,8 @@ def reduce_scatter_into(out: torch.Tensor, full: torch.Tensor, group, async_op: 
     if full.numel() != out.numel() * n:
         raise ValueError(f"reduce_scatter_into: full {full.numel()} != {n} x out {out.numel()}")
     w = dist.reduce_scatter_tensor(out.view(-1), full.reshape(-1), op=dist.ReduceOp.SUM, group=group,
-                                   async_op=async_op)
-    return w if async_op else Done()
+                                   async_op=True)
+    return _finish(w, async_op) if (async_op or _SERIALIZE) else (w.wait(), Done())[1]
 
 
 def gather_to_rank0(t: torch.Tensor, group=None) -> list[torch.Tensor] | None:

@@ -122,6 +122,8 @@ class FFNTrainer:
         self.T = T
         self.step_count = 0
         dev = self.device
+        if cfg.debug_sync:
+            comm.set_serialize(True)
 
         # ---- flat owned parameter layout (completion order) ------------------------------------
         full = {"w2": (D, self.F_loc), "w1": (self.R1, D)}

@@ -97,6 +97,7 @@ def run_rank(rank: int, world: int, cfg_dict: dict, method: int, backend: str, p
                 continue
             if i >= stop_after:
                 break
+            _maybe_inject_fault(rank, i)
             timer.start()
             x, dy = data.fill(int(s))
             eng.train_step(x, dy)
@@ -128,6 +129,21 @@ def run_rank(rank: int, world: int, cfg_dict: dict, method: int, backend: str, p
     if queue is not None and rank == 0:
         queue.put(("ok", to_numpy(rec)))  # by-value payload: survives the worker's exit
     return rec
+
+
+class InjectedFault(RuntimeError):
+    pass
+
+
+def _maybe_inject_fault(rank: int, step: int) -> None:
+    """Fault injection: ``DLLM_FAULT_RANK=k DLLM_FAULT_STEP=s`` makes rank k fail at step s
+    (``DLLM_FAULT_MODE=exit`` kills the process instead of raising) to test failure propagation."""
+    fr, fs = os.environ.get("DLLM_FAULT_RANK"), os.environ.get("DLLM_FAULT_STEP")
+    if fr is None or int(fr) != rank or int(fs or 0) != step:
+        return
+    if os.environ.get("DLLM_FAULT_MODE") == "exit":
+        os._exit(17)
+    raise InjectedFault(f"injected fault on rank {rank} at step {step}")
 
 
 def to_numpy(obj):

@@ -67,6 +67,7 @@ class TrainConfig:
     fused_optimizer: bool = True     # fuse SGD/Adam into the wgrad GEMM epilogue when no grad collective
     force_comm: bool = False         # run the DDP/FSDP collective path even at dp=1 (single-GPU RCCL check)
     comm_backend: str = "torch"      # torch (ProcessGroupNCCL/gloo) | native (csrc/comm.cpp RCCL layer)
+    debug_sync: bool = False         # race screen: wait every collective at issue + device sync per layer
 
     @property
     def tokens(self) -> int:
@@ -120,3 +121,5 @@ def add_extended_args(p: argparse.ArgumentParser) -> None:
     p.add_argument("--metrics_jsonl", default="")
     p.add_argument("--strict", action="store_true", help="exit non-zero when method results disagree")
     p.add_argument("--master_port", type=int, default=29500)
+    p.add_argument("--debug_sync", action="store_true",
+                   help="race screen: serialize every collective (must match the overlapped run bitwise)")

@@ -89,3 +89,20 @@ def test_dp_paths_match_single_device(pg, backend, dp_mode, opt):
     for g, w in zip(got, ref):
         for k in w:
             torch.testing.assert_close(g[k], w[k], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("backend", ["torch", "native"])
+@pytest.mark.parametrize("dp_mode", ["ddp", "zero", "fsdp"])
+def test_race_screen_serialized_equals_overlapped(pg, backend, dp_mode):
+    """SURVEY §5.2 race screen on the GPU: serialized collectives + device syncs == overlapped, bitwise."""
+    from dllm.parallel import comm
+
+    a = _run(dp_mode, backend, dtype="bf16")
+    comm.set_serialize(True)
+    try:
+        b = _run(dp_mode, backend, dtype="bf16")
+    finally:
+        comm.set_serialize(False)
+    for g, w in zip(a, b):
+        for k in w:
+            assert torch.equal(g[k], w[k]), (dp_mode, k)

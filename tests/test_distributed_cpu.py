@@ -155,3 +155,24 @@ def test_zero2_checkpoint_resume(tmp_path, free_port):
     ck = str(tmp_path / "z")
     _run(cfg, 6, 2, free_port + 1, ckpt_dir=ck, stop_after=1, ckpt_format="sharded")
     _close(_run(cfg, 6, 2, free_port + 2, resume=ck), full, rtol=1e-6, atol=1e-8)
+
+
+@pytest.mark.parametrize("mode", ["raise", "exit"])
+def test_injected_fault_fails_the_job(mode, free_port, monkeypatch):
+    """A rank dying mid-training must fail the whole job promptly (no hang on the peers' collectives)."""
+    monkeypatch.setenv("DLLM_FAULT_RANK", "1")
+    monkeypatch.setenv("DLLM_FAULT_STEP", "1")
+    monkeypatch.setenv("DLLM_FAULT_MODE", mode)
+    cfg = _cfg(L=2, steps=4)
+    with pytest.raises(RuntimeError):
+        spawn(2, cfg, 2, "gloo", free_port, {"seed": 1, "init": "cpu_compat"}, timeout_s=120)
+
+
+@pytest.mark.parametrize("method", [2, 3, 6])
+def test_serialized_streams_match_overlapped(method, free_port):
+    """Race screen: the fully serialized communication schedule gives bitwise-identical parameters."""
+    cfg = _cfg(L=3, steps=4)
+    a = _run(cfg, method, 2, free_port)
+    cfg_s = _cfg(L=3, steps=4, debug_sync=True)
+    b = _run(cfg_s, method, 2, free_port + 1)
+    _close(a, b, rtol=0, atol=0)
