@@ -22,6 +22,7 @@
 //    raster so blocks sharing operand panels run on one XCD's L2.
 //  * gemm_f32_128: exact-fp32 parity path (mfma_f32_16x16x4f32), 128x128x16 tile, register-staged.
 //  * gemm_generic: any shape / any dtype, bounds-checked FMA kernel (tests, odd TP shards).
+#include <algorithm>
 #include <type_traits>
 
 #include "common.h"
@@ -43,6 +44,8 @@ struct GemmArgs {
   float lr, b1, b2, eps, wd, bc1, bc2;
   float* opt_m;
   float* opt_v;
+  // split-K: ksplit > 1 -> the main kernel writes fp32 partials C + split*M*ldc (C = workspace)
+  int ksplit;
 };
 
 // ----------------------------------------------------------------------------------------------
@@ -418,7 +421,9 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wid >> 2, wc = wid & 3;
   const int tiles_m = p.M / BT_M, tiles_n = p.N / BT_N;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bid0 = xcd_remap(blockIdx.x, gridDim.x);
+  const int ntiles = tiles_m * tiles_n;
+  const int split = bid0 / ntiles, bid = bid0 % ntiles;  // split-K slice (0 when ksplit == 1)
   const int width = p.group_m * tiles_n;
   const int first_m = (bid / width) * p.group_m;
   const int gsz = min(tiles_m - first_m, p.group_m);
@@ -439,10 +444,11 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
   const long b_kstep = B_KC ? BT_K : (long)BT_K * p.ldb;
   const long a_hstep = A_KC ? 128L * p.lda : 128L;
   const long b_hstep = B_KC ? 128L * p.ldb : 128L;
-  const int nk = p.K / BT_K;  // even
+  const int nk = p.K / BT_K / p.ksplit;  // even (host guarantees (K/64) % (2*ksplit) == 0)
+  const int kt0 = split * nk;
 
   auto stage = [&](int op, int hh, int kt, int buf) {
-    kt = min(kt, nk - 1);
+    kt = kt0 + min(kt, nk - 1);
     DLLM_LDS char* dst = lds + ((op * 2 + hh) * 2 + buf) * HT;
     const uint16_t* src = op == 0 ? Ag + kt * a_kstep + hh * a_hstep : Bg + kt * b_kstep + hh * b_hstep;
     const long* off = op == 0 ? aoff : boff;
@@ -617,6 +623,9 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
   }
   // drain the clamped tail prefetches before the block can release its LDS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (EPI == EPI_STORE) {
+    if (p.ksplit > 1) p.C = (char*)p.C + (long)split * p.M * p.ldc * sizeof(OutT);
+  }
 
   // epilogue: quadrant (QM,QN), tile (mt,nt): lane holds C[m][n..n+3]
 #pragma unroll
@@ -847,13 +856,62 @@ __global__ void glu_combine(const T* h, long ldh, T* out, long ldo, int M, int F
 }
 
 // ----------------------------------------------------------------------------------------------
+// split-K reduction: sum the fp32 partials ws[0..S) and apply the real epilogue (any EPI / OutT)
+// ----------------------------------------------------------------------------------------------
+template <int EPI, typename OutT>
+__global__ __launch_bounds__(256) void splitk_reduce(GemmArgs p, const float* ws, int S) {
+  const long n4 = p.N / 4;
+  const long total = (long)p.M * n4;
+  const long plane = (long)p.M * p.N;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int m = (int)(i / n4), n = (int)(i % n4) * 4;
+    if constexpr (EPI == EPI_GLU) {
+      if ((n & 31) >= 16) continue;  // the gate block's thread handles the pair (n, n+16)
+      f32x4_t g = {0.f, 0.f, 0.f, 0.f}, u = {0.f, 0.f, 0.f, 0.f};
+      for (int s = 0; s < S; ++s) {
+        g += *(const f32x4_t*)(ws + s * plane + (long)m * p.N + n);
+        u += *(const f32x4_t*)(ws + s * plane + (long)m * p.N + n + 16);
+      }
+      epi_glu_pair<OutT>(p, m, (n >> 5) * 16 + (n & 15), n, n + 16, g, u);
+    } else {
+      f32x4_t v = {0.f, 0.f, 0.f, 0.f};
+      for (int s = 0; s < S; ++s) v += *(const f32x4_t*)(ws + s * plane + (long)m * p.N + n);
+      if constexpr (EPI == EPI_DGLU) epi_dglu<OutT>(p, m, n, v);
+      else epi4<EPI, OutT>(p, m, n, v);
+    }
+  }
+}
+
+// main kernel writes partials into the workspace, then the reduction applies the epilogue
+template <int L, int E>
+static hipError_t launch_splitk(const GemmArgs& a, int out_dt, float* ws, hipStream_t s) {
+  GemmArgs w = a;
+  w.C = ws;
+  w.ldc = a.N;
+  w.alpha = 1.f;
+  w.beta = 0.f;
+  const int nb = (a.M / BT_M) * (a.N / BT_N) * a.ksplit;
+  hipLaunchKernelGGL((gemm_bf16_8ph<L, EPI_STORE, float, true>), dim3(nb), dim3(512), 0, s, w);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  long n4 = (long)a.M * (a.N / 4);
+  int g = (int)std::min<long>((n4 + 255) / 256, 4096);
+  if (out_dt == DT_F32) hipLaunchKernelGGL((splitk_reduce<E, float>), dim3(g), dim3(256), 0, s, a, ws, a.ksplit);
+  else hipLaunchKernelGGL((splitk_reduce<E, uint16_t>), dim3(g), dim3(256), 0, s, a, ws, a.ksplit);
+  return hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------------------------
 // host dispatch
 // ----------------------------------------------------------------------------------------------
 // variant: 0 = auto (8-phase when K % 128 == 0, else 2-stage), 1 = 2-stage, 2 = 8-phase, 3 = 8-phase staggered
 static int g_bf16_variant = 0;
 
+static float* g_splitk_ws = nullptr;  // set per call by dllm_gemm (caller-owned workspace)
+
 template <int L, int E>
 static hipError_t launch_bf16(const GemmArgs& a, int out_dt, hipStream_t s) {
+  if (a.ksplit > 1) return launch_splitk<L, E>(a, out_dt, g_splitk_ws, s);
   const int nb = (a.M / BT_M) * (a.N / BT_N);
   int v = g_bf16_variant;
   if (v == 0) v = (a.K % (2 * BT_K) == 0) ? 3 : 1;
@@ -912,6 +970,7 @@ static hipError_t dispatch_epi(int path, int epi, const GemmArgs& a, int in_dt, 
 // weight-gradient GEMMs with a fused optimizer epilogue: TN layout, fp32 master output only
 template <int E>
 static hipError_t dispatch_opt(int path, const GemmArgs& a, int in_dt, hipStream_t s) {
+  if (path == 0 && a.ksplit > 1) return launch_splitk<L_TN, E>(a, DT_F32, g_splitk_ws, s);
   if (path == 0) {
     const int nb = (a.M / BT_M) * (a.N / BT_N);
     if (a.K % (2 * BT_K) == 0 && g_bf16_variant != 1)
@@ -938,7 +997,8 @@ extern "C" {
 int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const void* A, long lda,
               const void* B, long ldb, void* C, long ldc, const void* aux, void* aux_out, long ldaux,
               int M, int N, int K, float alpha, float beta, int group_m, int force_path, void* stream,
-              float lr, float b1, float b2, float eps, float wd, int step, float* opt_m, float* opt_v) {
+              float lr, float b1, float b2, float eps, float wd, int step, float* opt_m, float* opt_v,
+              int ksplit, float* workspace) {
   if (M <= 0 || N <= 0 || K <= 0) return -1;
   if (layout < 0 || layout > 2) return -1;
   if ((epi == EPI_GLU || epi == EPI_DGLU) && (N % 32) != 0) return -1;
@@ -949,6 +1009,7 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
   a.group_m = group_m > 0 ? group_m : 4;
   a.lr = lr; a.b1 = b1; a.b2 = b2; a.eps = eps; a.wd = wd; a.opt_m = opt_m; a.opt_v = opt_v;
   a.bc1 = 1.f; a.bc2 = 1.f;
+  a.ksplit = 1;
   const bool opt_epi = (epi == EPI_SGD || epi == EPI_ADAM);
   if (opt_epi && (layout != L_TN || out_dtype != DT_F32)) return -1;
   if (epi == EPI_ADAM) {
@@ -966,6 +1027,15 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
     path = force_path;
   }
   if (path == 2 && epi == EPI_GLU && aux_out == nullptr) return -1;
+  if (ksplit > 1) {
+    // split-K only on the bf16 8-phase path (each slice an even number of 64-deep K-tiles); a request
+    // that cannot be honoured (other kernel family / forced 2-stage variant) runs unsplit
+    if (workspace == nullptr) return -1;
+    if (path == 0 && (K / BT_K) % (2 * ksplit) == 0 && g_bf16_variant != 1) {
+      a.ksplit = ksplit;
+      g_splitk_ws = workspace;
+    }
+  }
   hipStream_t s = (hipStream_t)stream;
   hipError_t e;
   if (opt_epi) {

@@ -121,6 +121,43 @@ def _torch_gemm(a, b, layout, out, epi, act, aux, aux_out, alpha, beta, opt=None
     return out
 
 
+NUM_CUS = 256
+_SPLITK = {"enabled": True}
+
+
+def choose_ksplit(M: int, N: int, K: int) -> int:
+    """Split-K factor for the 256x256 bf16 kernel: raise CU occupancy when the tile grid is small.
+
+    One block per CU (128 KiB LDS), 256 CUs: pick the factor s (K-tiles per slice even, >= 8) that
+    maximises tiles*s / (waves*256), and only when it beats s = 1 by >= 25 % (the partials cost one
+    fp32 round trip through HBM)."""
+    if not _SPLITK["enabled"] or M % 256 or N % 256 or K % 128:
+        return 1
+    tiles = (M // 256) * (N // 256)
+    if tiles >= NUM_CUS * 0.75:
+        return 1
+
+    def util(s):
+        blocks = tiles * s
+        return blocks / (-(-blocks // NUM_CUS) * NUM_CUS)
+
+    best, best_u = 1, util(1)
+    for s in (2, 3, 4, 6, 8):
+        nkt = K // 64
+        if nkt % (2 * s) or nkt // s < 8:
+            continue
+        u = util(s)
+        if u > best_u * 1.25:
+            best, best_u = s, u
+    return best
+
+
+def set_splitk(enabled: bool) -> bool:
+    old = _SPLITK["enabled"]
+    _SPLITK["enabled"] = enabled
+    return old
+
+
 def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None = None, *, epi: str = "store",
          act: str = "none", aux: torch.Tensor | None = None, aux_out: torch.Tensor | None = None,
          alpha: float = 1.0, beta: float = 0.0, out_dtype: torch.dtype | None = None, group_m: int = 4,
@@ -163,6 +200,13 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
             raise TypeError("aux / aux_out must have the output dtype")
     L = _native.lib()
     in_dt, out_dt = _native.dtype_code(a.dtype), _native.dtype_code(out.dtype)
+    ksplit, ws = 1, None
+    if a.dtype == torch.bfloat16 and force in (None, "mfma_bf16"):
+        ksplit = choose_ksplit(M, N, K)
+        if ksplit > 1 and L.dllm_gemm_path(in_dt, out_dt, M, N, K, a.stride(0), b.stride(0), out.stride(0)) == 0:
+            ws = torch.empty(ksplit * M * N, dtype=torch.float32, device=a.device)
+        else:
+            ksplit = 1
     rc = L.dllm_gemm(in_dt, out_dt, LAYOUTS[layout], EPIS[epi], act_code(act),
                      a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), out.data_ptr(), out.stride(0),
                      aux.data_ptr() if aux is not None else None,
@@ -171,7 +215,8 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
                      M, N, K, float(alpha), float(beta), int(group_m), FORCE[force],
                      _native.stream_ptr(a.device), float(lr), float(betas[0]), float(betas[1]), float(eps),
                      float(wd), int(step), opt_m.data_ptr() if opt_m is not None else None,
-                     opt_v.data_ptr() if opt_v is not None else None)
+                     opt_v.data_ptr() if opt_v is not None else None, ksplit,
+                     ws.data_ptr() if ws is not None else None)
     _native.check(rc, f"dllm_gemm({layout},{epi},M={M},N={N},K={K})")
     return out
 

@@ -227,3 +227,48 @@ def test_streams_and_events_overlap():
     total = sum(outs)
     ref = sum(_ref(x.cpu(), y.cpu(), "nt") for x, y in zip(a, b))
     assert ((total.cpu().double() - ref).abs().max() / ref.abs().max()) < 1e-5
+
+
+@pytest.mark.parametrize("layout", ["nt", "nn", "tn"])
+@pytest.mark.parametrize("epi", ["store", "act", "dact", "glu", "dglu", "store_f32", "sgd", "adam"])
+def test_splitk_matches_unsplit(layout, epi):
+    """Split-K (fp32 partials + reduction epilogue) on a small tile grid == the single-pass kernel."""
+    from dllm.ops.gemm import choose_ksplit, set_splitk
+
+    M, N, K = 512, 512, 2048   # 4 tiles -> split 8
+    if epi in ("sgd", "adam") and layout != "tn":
+        pytest.skip("optimizer epilogues are weight-gradient (TN) only")
+    assert choose_ksplit(M, N, K) > 1
+    a, b = _operands(layout, M, N, K, torch.bfloat16, seed=31)
+    a, b = a.cuda(), b.cuda()
+    res = []
+    for split in (False, True):
+        set_splitk(split)
+        kw = {}
+        if epi in ("store", "act", "dact", "glu", "dglu"):
+            ncols = {"glu": N // 2, "dglu": 2 * N}.get(epi, N)
+            out = torch.zeros(M, ncols, dtype=torch.bfloat16, device="cuda")
+            if epi == "act":
+                kw = dict(epi="act", act="gelu", aux_out=torch.zeros(M, N, dtype=torch.bfloat16, device="cuda"))
+            elif epi == "dact":
+                kw = dict(epi="dact", act="silu", aux=_mk((M, N), torch.bfloat16, 5).cuda())
+            elif epi == "glu":
+                kw = dict(epi="glu", act="silu", aux_out=torch.zeros(M, N, dtype=torch.bfloat16, device="cuda"))
+            elif epi == "dglu":
+                kw = dict(epi="dglu", act="silu", aux=_mk((M, 2 * N), torch.bfloat16, 6).cuda())
+        elif epi == "store_f32":
+            out = _mk((M, N), torch.float32, 8).cuda()
+            kw = dict(beta=1.0)
+        else:
+            out = _mk((M, N), torch.float32, 9).cuda()
+            kw = dict(epi=epi, lr=1e-3, aux_out=torch.zeros(M, N, dtype=torch.bfloat16, device="cuda"))
+            if epi == "adam":
+                kw.update(step=2, opt_m=torch.full((M, N), 0.01, device="cuda"),
+                          opt_v=torch.full((M, N), 1e-4, device="cuda"))
+        gemm(a, b, layout, out=out, **kw)
+        torch.cuda.synchronize()
+        res.append([out] + [v for v in kw.values() if isinstance(v, torch.Tensor)])
+    set_splitk(True)
+    for x, y in zip(*res):
+        tol = 2e-2 if x.dtype == torch.bfloat16 else 1e-5
+        torch.testing.assert_close(x.float(), y.float(), rtol=tol, atol=tol * float(y.float().abs().max() + 1e-30))
