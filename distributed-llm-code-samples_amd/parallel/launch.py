@@ -91,15 +91,19 @@ def run_rank(rank: int, world: int, cfg_dict: dict, method: int, backend: str, p
     timer = StepTimer(device)
     stop_after = int(opts.get("stop_after") or len(my_seeds))
     done = start_step
+    seed_list = my_seeds.tolist()
+    if start_step < len(seed_list):
+        data.prefetch(int(seed_list[start_step]))
     with maybe_profile(opts.get("profile", ""), rank):
-        for i, s in enumerate(my_seeds.tolist()):
+        for i, s in enumerate(seed_list):
             if i < start_step:
                 continue
             if i >= stop_after:
                 break
             _maybe_inject_fault(rank, i)
             timer.start()
-            x, dy = data.fill(int(s))
+            nxt = seed_list[i + 1] if i + 1 < min(len(seed_list), stop_after) else None
+            x, dy = data.fill(int(s), next_seed=nxt)
             eng.train_step(x, dy)
             timer.stop()
             done = i + 1
