@@ -168,6 +168,275 @@ __device__ __forceinline__ void epi_dglu(const GemmArgs& p, int m, int n_da, f32
 }
 
 // ----------------------------------------------------------------------------------------------
+// Batched epilogue of the 256x256 8-phase kernel.
+//
+// The per-element helpers above are fine for the elementwise split-K reduction, but inside the GEMM
+// they serialise: hipcc cannot prove that a store to C (or aux_out) does not alias the NEXT group's
+// load of C / aux, so every 4-column group became load -> s_waitcnt vmcnt(0) -> math -> store, i.e.
+// 32 exposed HBM round trips per tile (measured: +105 us on a 1.1-TFLOP fused-SGD wgrad, +110 us on
+// the act'-masked dgrad).  Here each wave issues all loads of a batch of row groups first (batch size
+// chosen to keep <= 64 extra VGPRs live next to the 128 accumulators), then the math and stores, so a
+// tile pays 1-8 round trips.  Optional side outputs (aux_out) are written under ONE uniform branch per
+// batch.  ACT >= 0 selects the activation at compile time (no per-element switch: the runtime-switch
+// build of the act epilogue was ~14k instructions, larger than the instruction cache).
+// ----------------------------------------------------------------------------------------------
+template <int ACT> __device__ __forceinline__ float actf(int rt, float x) { return act_fwd(ACT < 0 ? rt : ACT, x); }
+template <int ACT> __device__ __forceinline__ float actg(int rt, float x) { return act_grad(ACT < 0 ? rt : ACT, x); }
+
+template <typename T> struct Raw4;
+template <> struct Raw4<uint16_t> {
+  using type = uint2;
+  static __device__ __forceinline__ type load(const void* b, long i) { return *(const uint2*)((const uint16_t*)b + i); }
+  static __device__ __forceinline__ f32x4_t cvt(type u) {
+    return f32x4_t{bf2f(u.x & 0xffff), bf2f(u.x >> 16), bf2f(u.y & 0xffff), bf2f(u.y >> 16)};
+  }
+};
+template <> struct Raw4<float> {
+  using type = f32x4_t;
+  static __device__ __forceinline__ type load(const void* b, long i) { return *(const f32x4_t*)((const float*)b + i); }
+  static __device__ __forceinline__ f32x4_t cvt(type u) { return u; }
+};
+
+// row groups per batch for `cost` extra VGPRs per row group (<= 64 extra live VGPRs)
+constexpr int epi_batch(int cost) {
+  return cost == 0 ? 16 : (64 / cost >= 16 ? 16 : 64 / cost >= 8 ? 8 : 64 / cost >= 4 ? 4 : 64 / cost >= 2 ? 2 : 1);
+}
+
+// Paired 16-B bf16 access (guide T21 pattern, with v_permlane16_swap): a lane's 4 columns of the
+// nt = 0 fragment (a) and of the nt = 1 fragment (b) of one row are exchanged with the lane 16 away so
+// that lanes 16g..16g+15 hold 8 contiguous columns at pair_col(lane) = 16*(g&1) + 8*(g>>1) of the
+// 32-column wave strip.  One dwordx4 store replaces two dwordx2 (the epilogue store tail is
+// issue-bound); loads use the same map and the inverse (identical) exchange.
+__device__ __forceinline__ int pair_col(int lane) { return 16 * ((lane >> 4) & 1) + 8 * (lane >> 5); }
+__device__ __forceinline__ uint2 pk_bf16(f32x4_t v) {
+  return uint2{(uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16), (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16)};
+}
+__device__ __forceinline__ uint4 pair_swap(uint2 a, uint2 b) {
+  const auto x = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
+  const auto y = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
+  return uint4{x[0], y[0], x[1], y[1]};
+}
+__device__ __forceinline__ void st_pair_bf16(void* base, long idx, f32x4_t a, f32x4_t b) {
+  *(uint4*)((uint16_t*)base + idx) = pair_swap(pk_bf16(a), pk_bf16(b));
+}
+__device__ __forceinline__ void unpair_bf16(uint4 v, f32x4_t& a, f32x4_t& b) {
+  const uint4 u = pair_swap(uint2{v.x, v.y}, uint2{v.z, v.w});
+  a = Raw4<uint16_t>::cvt(uint2{u.x, u.y});
+  b = Raw4<uint16_t>::cvt(uint2{u.z, u.w});
+}
+
+// acc[QM][QN][mt][nt]: lane holds C[m0 + QM*128 + wr*64 + mt*16 + (lane&15)][n0 + QN*128 + wc*32 + nt*16 + 4*(lane>>4) + 0..3]
+// row group rg = QM*8 + QN*4 + mt (16 per wave), 2 column groups (nt) each.
+template <int EPI, typename OutT, int ACT>
+__device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2][2][4][2], int m0, int n0,
+                                             int wr, int wc, int lane) {
+  constexpr bool BF = std::is_same<OutT, uint16_t>::value;
+  using R = Raw4<OutT>;
+  using RT = typename std::conditional<BF, uint4, f32x4_t>::type;  // bf16: one paired 16-B load per row group
+  using RF = Raw4<float>;
+  constexpr int WR = BF ? 4 : 8;  // VGPRs per row group and loaded operand
+  constexpr int COST = EPI == EPI_DACT ? WR : EPI == EPI_DGLU ? 8 * (BF ? 2 : 4) : EPI == EPI_STORE ? WR
+                     : EPI == EPI_SGD ? 8 : EPI == EPI_ADAM ? 24 : 0;
+  constexpr int RB = epi_batch(COST);
+  const int pc = pair_col(lane);
+#define DLLM_M(rg) (m0 + ((rg) >> 3) * 128 + wr * 64 + ((rg) & 3) * 16 + (lane & 15))
+#define DLLM_NB(rg) (n0 + (((rg) >> 2) & 1) * 128 + wc * 32)
+#define DLLM_N(rg, nt) (DLLM_NB(rg) + (nt) * 16 + 4 * (lane >> 4))
+#define DLLM_ACC(rg, nt) acc[(rg) >> 3][((rg) >> 2) & 1][(rg) & 3][nt]
+  // store the row group's two fragments (already epilogue-transformed) to a [*, ld] OutT matrix
+  auto store_rg = [&](void* base, long ld, int m, int nb, f32x4_t a, f32x4_t b) {
+    if constexpr (BF) {
+      st_pair_bf16(base, (long)m * ld + nb + pc, a, b);
+    } else {
+      Vec4<float>::store(base, (long)m * ld + nb + 4 * (lane >> 4), a);
+      Vec4<float>::store(base, (long)m * ld + nb + 16 + 4 * (lane >> 4), b);
+    }
+  };
+  // load the row group's two fragments (raw) / decode them
+  auto load_rg = [&](const void* base, long ld, int m, int nb, RT (&dst)[2]) {
+    if constexpr (BF) {
+      dst[0] = *(const uint4*)((const uint16_t*)base + (long)m * ld + nb + pc);
+    } else {
+      dst[0] = RF::load(base, (long)m * ld + nb + 4 * (lane >> 4));
+      dst[1] = RF::load(base, (long)m * ld + nb + 16 + 4 * (lane >> 4));
+    }
+  };
+  auto decode_rg = [&](const RT (&src)[2], f32x4_t& a, f32x4_t& b) {
+    if constexpr (BF) unpair_bf16(src[0], a, b);
+    else { a = src[0]; b = src[1]; }
+  };
+  if constexpr (EPI == EPI_STORE) {
+    if (p.beta == 0.f) {
+#pragma unroll
+      for (int rg = 0; rg < 16; ++rg)
+        store_rg(p.C, p.ldc, DLLM_M(rg), DLLM_NB(rg), DLLM_ACC(rg, 0) * p.alpha, DLLM_ACC(rg, 1) * p.alpha);
+    } else {
+#pragma unroll
+      for (int b0 = 0; b0 < 16; b0 += RB) {
+        RT L[RB][2];
+#pragma unroll
+        for (int r = 0; r < RB; ++r) load_rg(p.C, p.ldc, DLLM_M(b0 + r), DLLM_NB(b0 + r), L[r]);
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          f32x4_t c0, c1;
+          decode_rg(L[r], c0, c1);
+          store_rg(p.C, p.ldc, DLLM_M(b0 + r), DLLM_NB(b0 + r), DLLM_ACC(b0 + r, 0) * p.alpha + p.beta * c0,
+                   DLLM_ACC(b0 + r, 1) * p.alpha + p.beta * c1);
+        }
+      }
+    }
+  } else if constexpr (EPI == EPI_ACT) {
+    if (p.aux_out) {
+#pragma unroll
+      for (int rg = 0; rg < 16; ++rg)
+        store_rg(p.aux_out, p.ldaux, DLLM_M(rg), DLLM_NB(rg), DLLM_ACC(rg, 0), DLLM_ACC(rg, 1));
+    }
+#pragma unroll
+    for (int rg = 0; rg < 16; ++rg) {
+      f32x4_t a = DLLM_ACC(rg, 0), b = DLLM_ACC(rg, 1);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a[e] = actf<ACT>(p.act, a[e]);
+        b[e] = actf<ACT>(p.act, b[e]);
+      }
+      store_rg(p.C, p.ldc, DLLM_M(rg), DLLM_NB(rg), a, b);
+    }
+  } else if constexpr (EPI == EPI_DACT) {
+#pragma unroll
+    for (int b0 = 0; b0 < 16; b0 += RB) {
+      RT H[RB][2];
+#pragma unroll
+      for (int r = 0; r < RB; ++r) load_rg(p.aux, p.ldaux, DLLM_M(b0 + r), DLLM_NB(b0 + r), H[r]);
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        f32x4_t h0, h1;
+        decode_rg(H[r], h0, h1);
+        f32x4_t a = DLLM_ACC(b0 + r, 0), b = DLLM_ACC(b0 + r, 1);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          a[e] *= actg<ACT>(p.act, h0[e]);
+          b[e] *= actg<ACT>(p.act, h1[e]);
+        }
+        store_rg(p.C, p.ldc, DLLM_M(b0 + r), DLLM_NB(b0 + r), a, b);
+      }
+    }
+  } else if constexpr (EPI == EPI_GLU) {
+    // gate / up 16-column blocks alternate: nt = 0 gate, nt = 1 up (same lane)
+    if (p.aux_out) {
+#pragma unroll
+      for (int rg = 0; rg < 16; ++rg)
+        store_rg(p.aux_out, p.ldaux, DLLM_M(rg), DLLM_NB(rg), DLLM_ACC(rg, 0), DLLM_ACC(rg, 1));
+    }
+#pragma unroll
+    for (int rg = 0; rg < 16; ++rg) {
+      const int nb = DLLM_N(rg, 0);
+      const f32x4_t g = DLLM_ACC(rg, 0), u = DLLM_ACC(rg, 1);
+      f32x4_t a;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a[e] = actf<ACT>(p.act, g[e]) * u[e];
+      Vec4<OutT>::store(p.C, (long)DLLM_M(rg) * p.ldc + (nb >> 5) * 16 + (nb & 15), a);
+    }
+  } else if constexpr (EPI == EPI_DGLU) {
+    // acc = da over the de-interleaved F axis; aux / C interleaved [g|u] 16-column blocks
+    using RD = typename R::type;
+#pragma unroll
+    for (int b0 = 0; b0 < 16; b0 += RB) {
+      RD G[RB][2], U[RB][2];
+#pragma unroll
+      for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const int nd = DLLM_N(b0 + r, nt), ng = (nd >> 4) * 32 + (nd & 15);
+          const long base = (long)DLLM_M(b0 + r) * p.ldaux + ng;
+          G[r][nt] = R::load(p.aux, base);
+          U[r][nt] = R::load(p.aux, base + 16);
+        }
+#pragma unroll
+      for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const int nd = DLLM_N(b0 + r, nt), ng = (nd >> 4) * 32 + (nd & 15);
+          const f32x4_t da = DLLM_ACC(b0 + r, nt), g = R::cvt(G[r][nt]), u = R::cvt(U[r][nt]);
+          f32x4_t dg, du;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            du[e] = da[e] * actf<ACT>(p.act, g[e]);
+            dg[e] = da[e] * u[e] * actg<ACT>(p.act, g[e]);
+          }
+          const long base = (long)DLLM_M(b0 + r) * p.ldc + ng;
+          Vec4<OutT>::store(p.C, base, dg);
+          Vec4<OutT>::store(p.C, base + 16, du);
+        }
+    }
+  } else if constexpr (EPI == EPI_SGD) {
+#pragma unroll
+    for (int b0 = 0; b0 < 16; b0 += RB) {
+      f32x4_t W[RB][2];
+#pragma unroll
+      for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) W[r][nt] = RF::load(p.C, (long)DLLM_M(b0 + r) * p.ldc + DLLM_N(b0 + r, nt));
+#pragma unroll
+      for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const f32x4_t g = DLLM_ACC(b0 + r, nt);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            W[r][nt][e] = __fadd_rn(W[r][nt][e], __fmul_rn(-p.lr, __fmul_rn(p.alpha, g[e])));
+          Vec4<float>::store(p.C, (long)DLLM_M(b0 + r) * p.ldc + DLLM_N(b0 + r, nt), W[r][nt]);
+        }
+      if (p.aux_out) {
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+          st_pair_bf16(p.aux_out, (long)DLLM_M(b0 + r) * p.ldaux + DLLM_NB(b0 + r) + pc, W[r][0], W[r][1]);
+      }
+    }
+  } else if constexpr (EPI == EPI_ADAM) {
+#pragma unroll
+    for (int b0 = 0; b0 < 16; b0 += RB) {
+      f32x4_t W[RB][2], Mm[RB][2], Vv[RB][2];
+#pragma unroll
+      for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const long ci = (long)DLLM_M(b0 + r) * p.ldc + DLLM_N(b0 + r, nt);
+          W[r][nt] = RF::load(p.C, ci);
+          Mm[r][nt] = RF::load(p.opt_m, ci);
+          Vv[r][nt] = RF::load(p.opt_v, ci);
+        }
+#pragma unroll
+      for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const f32x4_t gg = DLLM_ACC(b0 + r, nt);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float g = p.alpha * gg[e];
+            Mm[r][nt][e] = p.b1 * Mm[r][nt][e] + (1.f - p.b1) * g;
+            Vv[r][nt][e] = p.b2 * Vv[r][nt][e] + (1.f - p.b2) * g * g;
+            const float mh = Mm[r][nt][e] / p.bc1, vh = Vv[r][nt][e] / p.bc2;
+            W[r][nt][e] = W[r][nt][e] - p.lr * (mh / (sqrtf(vh) + p.eps) + p.wd * W[r][nt][e]);
+          }
+          const long ci = (long)DLLM_M(b0 + r) * p.ldc + DLLM_N(b0 + r, nt);
+          Vec4<float>::store(p.C, ci, W[r][nt]);
+          Vec4<float>::store(p.opt_m, ci, Mm[r][nt]);
+          Vec4<float>::store(p.opt_v, ci, Vv[r][nt]);
+        }
+      if (p.aux_out) {
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+          st_pair_bf16(p.aux_out, (long)DLLM_M(b0 + r) * p.ldaux + DLLM_NB(b0 + r) + pc, W[r][0], W[r][1]);
+      }
+    }
+  }
+#undef DLLM_M
+#undef DLLM_NB
+#undef DLLM_N
+#undef DLLM_ACC
+}
+
+// ----------------------------------------------------------------------------------------------
 // bf16 256x256x64 MFMA kernel
 // ----------------------------------------------------------------------------------------------
 constexpr int BT_M = 256, BT_N = 256, BT_K = 64;
@@ -411,7 +680,8 @@ __device__ __forceinline__ bf16x8_t cat_tr(s16x4_t lo, s16x4_t hi) {
 // ABL (ablation builds only; 0 in production): bit0/1 force K-contiguous LOADS of A/B, bit2/3 force
 // K-contiguous fragment READS of A/B, independent of LAYOUT (wrong results, same work) -- isolates the
 // cost of MN-contiguous LDS-DMA patterns vs transposed ds_read_b64_tr_b16 fragment reads.
-template <int LAYOUT, int EPI, typename OutT, bool STAGGER, int ABL = 0>
+// ACT >= 0: activation of the ACT/DACT/GLU/DGLU epilogues fixed at compile time (-1: runtime p.act)
+template <int LAYOUT, int EPI, typename OutT, bool STAGGER, int ABL = 0, int ACT = -1>
 __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
   // slot(op, hh, buf) = ((op*2 + hh)*2 + buf) * 16 KiB: A in [0, 64K), B in [64K, 128K), so every
   // fragment read is base + a 16-bit immediate
@@ -627,26 +897,7 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
     if (p.ksplit > 1) p.C = (char*)p.C + (long)split * p.M * p.ldc * sizeof(OutT);
   }
 
-  // epilogue: quadrant (QM,QN), tile (mt,nt): lane holds C[m][n..n+3]
-#pragma unroll
-  for (int QM = 0; QM < 2; ++QM)
-#pragma unroll
-    for (int QN = 0; QN < 2; ++QN)
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        const int m = m0 + QM * 128 + wr * 64 + mt * 16 + (lane & 15);
-        const int nb = n0 + QN * 128 + wc * 32 + 4 * (lane >> 4);
-        if constexpr (EPI == EPI_GLU) {
-          const int nc_out = (nb >> 5) * 16 + (nb & 15);
-          epi_glu_pair<OutT>(p, m, nc_out, nb, nb + 16, acc[QM][QN][mt][0], acc[QM][QN][mt][1]);
-        } else if constexpr (EPI == EPI_DGLU) {
-#pragma unroll
-          for (int nt = 0; nt < 2; ++nt) epi_dglu<OutT>(p, m, nb + nt * 16, acc[QM][QN][mt][nt]);
-        } else {
-#pragma unroll
-          for (int nt = 0; nt < 2; ++nt) epi4<EPI, OutT>(p, m, nb + nt * 16, acc[QM][QN][mt][nt]);
-        }
-      }
+  epilogue_256<EPI, OutT, ACT>(p, acc, m0, n0, wr, wc, lane);
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -909,6 +1160,23 @@ static int g_bf16_variant = 0;
 
 static float* g_splitk_ws = nullptr;  // set per call by dllm_gemm (caller-owned workspace)
 
+// staggered 8-phase launch; the FFN's own activation epilogues (NT act/glu forward, NN dact/dglu
+// dgrad, bf16 out) get a compile-time activation, everything else the runtime switch
+template <int L, int E, typename OutT>
+static void launch_8ph_stagger(const GemmArgs& a, int nb, hipStream_t s) {
+  constexpr bool fwd = L == L_NT && (E == EPI_ACT || E == EPI_GLU);
+  constexpr bool bwd = L == L_NN && (E == EPI_DACT || E == EPI_DGLU);
+  if constexpr ((fwd || bwd) && std::is_same<OutT, uint16_t>::value) {
+    switch (a.act) {
+      case ACT_RELU: hipLaunchKernelGGL((gemm_bf16_8ph<L, E, OutT, true, 0, ACT_RELU>), dim3(nb), dim3(512), 0, s, a); return;
+      case ACT_SILU: hipLaunchKernelGGL((gemm_bf16_8ph<L, E, OutT, true, 0, ACT_SILU>), dim3(nb), dim3(512), 0, s, a); return;
+      case ACT_GELU: hipLaunchKernelGGL((gemm_bf16_8ph<L, E, OutT, true, 0, ACT_GELU>), dim3(nb), dim3(512), 0, s, a); return;
+      default: break;
+    }
+  }
+  hipLaunchKernelGGL((gemm_bf16_8ph<L, E, OutT, true>), dim3(nb), dim3(512), 0, s, a);
+}
+
 template <int L, int E>
 static hipError_t launch_bf16(const GemmArgs& a, int out_dt, hipStream_t s) {
   if (a.ksplit > 1) return launch_splitk<L, E>(a, out_dt, g_splitk_ws, s);
@@ -924,8 +1192,8 @@ static hipError_t launch_bf16(const GemmArgs& a, int out_dt, hipStream_t s) {
     if (f32) hipLaunchKernelGGL((gemm_bf16_8ph<L, E, float, false>), dim3(nb), dim3(512), 0, s, a);
     else hipLaunchKernelGGL((gemm_bf16_8ph<L, E, uint16_t, false>), dim3(nb), dim3(512), 0, s, a);
   } else {
-    if (f32) hipLaunchKernelGGL((gemm_bf16_8ph<L, E, float, true>), dim3(nb), dim3(512), 0, s, a);
-    else hipLaunchKernelGGL((gemm_bf16_8ph<L, E, uint16_t, true>), dim3(nb), dim3(512), 0, s, a);
+    if (f32) launch_8ph_stagger<L, E, float>(a, nb, s);
+    else launch_8ph_stagger<L, E, uint16_t>(a, nb, s);
   }
   return hipGetLastError();
 }
