@@ -79,10 +79,14 @@ def run_rank(rank: int, world: int, cfg_dict: dict, method: int, backend: str, p
                       device=device if device.type == "cuda" else None)
     eng = FFNTrainer(cfg, mesh, device)
 
-    seed = int(opts["seed"])
+    seed = int(opts.get("seed", 0))
     init = opts.get("init", "cpu_compat")
-    eng.load_full_params(build_params(cfg, init, seed, device))
-    seeds = draw_seeds(cfg, seed)
+    if opts.get("params") is not None:  # caller-provided logical parameters (api.train_* entry points)
+        eng.load_full_params([{k: torch.as_tensor(v) for k, v in p.items()} for p in opts["params"]])
+    else:
+        eng.load_full_params(build_params(cfg, init, seed, device))
+    seeds = torch.as_tensor(opts["seeds"], dtype=torch.int64) if opts.get("seeds") is not None \
+        else draw_seeds(cfg, seed)
     my_seeds = stripe_seeds(seeds, dp, mesh.dp_rank) if dp > 1 else seeds
     start_step = 0
     if opts.get("resume"):
