@@ -33,7 +33,7 @@ from dllm.parallel.engine import FFNTrainer
 from dllm.parallel.mesh import Mesh, init_distributed
 from dllm.utils.config import ModelConfig, TrainConfig
 from dllm.utils.data import DeviceMockData
-from dllm.utils.metrics import flops_per_step
+from dllm.utils.metrics import PEAK_TFLOPS, flops_per_step
 
 METRIC = "FFN tokens/sec (whole node) at hidden=4096 for DDP/FSDP/MP, 1/2/4/8 MI355X"
 
@@ -152,6 +152,7 @@ def main() -> int:
     value = tokens_global * a.steps / el
     tflops = flops_per_step(cfg, tp=tp, recompute=cfg.recompute) / (ms / 1e3) / 1e12
     finite = bool(torch.isfinite(eng.master[:1024]).all().item())
+    peak_gib = 0.0 if cpu else torch.cuda.max_memory_allocated(dev) / 2**30
     if eng.zero:
         eng.zero_sync_state()  # quiesce in-flight weight all-gathers before teardown
     par = {"ddp": f"dp{n}", "zero": f"dp{n}-zero2", "fsdp": f"fsdp{n}", "tp": f"tp{n}",
@@ -164,7 +165,8 @@ def main() -> int:
         "config": {"model": f"ffn-stack L{m.layers} D{m.D} F{m.F} {'swiglu-' if m.gated else ''}{m.act}",
                    "global_batch": a.batch_size * dp, "seq_len": a.seq_len, "parallelism": par,
                    "optimizer": a.optimizer, "grad_dtype": a.grad_dtype, "master_weights": "fp32"},
-        "tflops_per_gpu": round(tflops, 1), "finite": finite, "comm": a.comm, "hip_graph": bool(a.graph),
+        "tflops_per_gpu": round(tflops, 1), "mfu_dense": round(tflops / PEAK_TFLOPS[a.dtype], 4),
+        "peak_hbm_gib": round(peak_gib, 2), "finite": finite, "comm": a.comm, "hip_graph": bool(a.graph),
     }
     if a.force_comm:
         rec["note"] = "force_comm: DDP/FSDP collectives over size-1 RCCL communicators"

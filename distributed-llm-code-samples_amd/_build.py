@@ -80,12 +80,42 @@ def _compile(src: str, verbose: bool) -> str:
     return obj
 
 
+TOOLS = os.path.join(CSRC, "tools")
+BIN = os.path.join(PKG_DIR, "bin")
+
+
+def build_tools(verbose: bool = False, force: bool = False) -> list[str]:
+    """Standalone native executables (``csrc/tools/*.cpp`` -> ``bin/dllm_<name>``): separate processes
+    without torch, so they link ROCm's own HIP runtime and RCCL."""
+    if not os.path.isdir(TOOLS):
+        return []
+    os.makedirs(BIN, exist_ok=True)
+    out = []
+    for f in sorted(os.listdir(TOOLS)):
+        if not f.endswith(".cpp"):
+            continue
+        src = os.path.join(TOOLS, f)
+        exe = os.path.join(BIN, "dllm_" + f[:-4])
+        out.append(exe)
+        if not force and os.path.exists(exe) and os.path.getmtime(exe) >= os.path.getmtime(src):
+            continue
+        cmd = [_hipcc(), "-O2", "-std=c++17", f"--offload-arch={ARCH}", "-x", "hip", src, "-o", exe,
+               f"-L{ROCM}/lib", "-lrccl", f"-Wl,-rpath,{ROCM}/lib"]
+        if verbose:
+            print("[dllm build]", " ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
+    return out
+
+
 def build(verbose: bool = False, force: bool = False, jobs: int = 4) -> str:
     """Compile all native sources for gfx950 and link ``_dllm_native.so``; returns the library path."""
     os.makedirs(BUILD, exist_ok=True)
     if force:
         for f in os.listdir(BUILD):
             os.remove(os.path.join(BUILD, f))
+    build_tools(verbose, force)
     srcs = sources()
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         objs = list(ex.map(lambda s: _compile(s, verbose), srcs))

@@ -127,6 +127,7 @@ def run_rank(rank: int, world: int, cfg_dict: dict, method: int, backend: str, p
             "shapes": [(tuple(p["w1"].shape), tuple(p["w2"].shape)) for p in full] if full else None,
             "slices": [(p["w1"][:5, :5].clone(), p["w2"][:5, :5].clone()) for p in full] if full else None,
             "params": full if opts.get("return_full", False) else None,
+            "peak_hbm_gib": torch.cuda.max_memory_allocated(device) / 2**30 if device.type == "cuda" else 0.0,
         }
     if world > 1 or opts.get("force_dist"):
         import torch.distributed as dist

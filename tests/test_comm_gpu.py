@@ -106,3 +106,23 @@ def test_race_screen_serialized_equals_overlapped(pg, backend, dp_mode):
     for g, w in zip(a, b):
         for k in w:
             assert torch.equal(g[k], w[k]), (dp_mode, k)
+
+
+def test_native_single_process_rccl_selftest():
+    """test_nccl.py analog: ncclCommInitAll over every visible device, group-fused AG/AR/RS of 128 fp32
+    per rank against host expectations (csrc/tools/rccl_selftest.cpp)."""
+    import os
+    import subprocess
+
+    import dllm
+    from dllm import _build
+
+    exe = os.path.join(_build.BIN, "dllm_rccl_selftest")
+    if not os.path.exists(exe):
+        _build.build_tools()
+    env = dict(os.environ)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=180, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "PASSED" in r.stdout
+    for op in ("all_gather ok", "all_reduce ok", "reduce_scatter ok"):
+        assert op in r.stdout
