@@ -88,12 +88,16 @@ def needs_preact(act: str, gated: bool) -> bool:
 
 
 def layer_fwd(x: torch.Tensor, w1: torch.Tensor, w2: torch.Tensor, act: str, gated: bool,
-              a_out: torch.Tensor, h_out: torch.Tensor | None, y_out: torch.Tensor) -> torch.Tensor:
-    """y = act(x·W1ᵀ)·W2ᵀ  (gated: (act(x·W1ᵀ)⊙x·W3ᵀ)·W2ᵀ with ``w1`` = interleaved W13)."""
+              a_out: torch.Tensor, h_out: torch.Tensor | None, y_out: torch.Tensor,
+              before_fwd2=None) -> torch.Tensor:
+    """y = act(x·W1ᵀ)·W2ᵀ  (gated: (act(x·W1ᵀ)⊙x·W3ᵀ)·W2ᵀ with ``w1`` = interleaved W13).
+    ``before_fwd2()`` runs between the two GEMMs (e.g. waiting for W2's all-gather)."""
     if gated:
         gemm(x, w1, "nt", out=a_out, epi="glu", act=act, aux_out=h_out)
     else:
         gemm(x, w1, "nt", out=a_out, epi="act", act=act, aux_out=h_out)
+    if before_fwd2 is not None:
+        before_fwd2()
     gemm(a_out, w2, "nt", out=y_out)
     return y_out
 
@@ -109,13 +113,25 @@ def layer_bwd(dy: torch.Tensor, x: torch.Tensor, w1: torch.Tensor, w2: torch.Ten
 
     Order ``da, dW2, dx, dW1``: every dgrad that reads a weight runs before that weight's (possibly fused)
     update, a TP all-reduce of ``dx`` overlaps the dW1 GEMM, and ``hooks`` (``after_w2``, ``after_dx``,
-    ``after_w1``) mark the points where gradient collectives can be issued.
+    ``after_w1``) mark the points where gradient collectives can be issued.  Without ``dx`` (layer 0)
+    the order is ``da, dW1, dW2`` (the engine's flat layout follows the completion order).
     """
     if gated:
         gemm(dy, w2, "nn", out=da_buf, epi="dglu", act=act, aux=h)    # [dg|du] interleaved [T, 2F]
     else:
         gemm(dy, w2, "nn", out=da_buf, epi="dact", act=act, aux=h if h is not None else a)
+    kw1 = gw1 if isinstance(gw1, dict) else {"out": gw1}
     kw2 = gw2 if isinstance(gw2, dict) else {"out": gw2}
+    if dx_out is None:
+        # no input gradient (layer 0): dW1 first, so W1's gradient collective / update starts while dW2
+        # runs and the next forward's first GEMM (which needs W1) is not behind the step's last collective
+        gemm(da_buf, x, "tn", **kw1)                                  # dW1 = daᵀ·x        [F, D]
+        if hooks is not None:
+            hooks.after_w1()
+        gemm(dy, a, "tn", **kw2)                                      # dW2 = dyᵀ·a        [D, F]
+        if hooks is not None:
+            hooks.after_w2()
+        return None
     gemm(dy, a, "tn", **kw2)                                          # dW2 = dyᵀ·a        [D, F]
     if hooks is not None:
         hooks.after_w2()
@@ -124,7 +140,6 @@ def layer_bwd(dy: torch.Tensor, x: torch.Tensor, w1: torch.Tensor, w2: torch.Ten
         dx = gemm(da_buf, w1, "nn", out=dx_out)                       # dx = da·W1         [T, D]
         if hooks is not None:
             hooks.after_dx(dx)
-    kw1 = gw1 if isinstance(gw1, dict) else {"out": gw1}
     gemm(da_buf, x, "tn", **kw1)                                      # dW1 = daᵀ·x        [F, D]
     if hooks is not None:
         hooks.after_w1()

@@ -131,8 +131,13 @@ class FFNTrainer:
         off = 0
         # ZeRO shards every bucket evenly over dp ranks: keep every entry a multiple of dp*ALIGN
         self.align = ALIGN * d if self.zero else ALIGN
+        # layer 0 without an input gradient finishes dW1 BEFORE dW2 (see layer_bwd): its W1 gradient is
+        # reduced, updated and re-gathered while the last GEMM (dW2) still runs, and the next forward's
+        # first GEMM needs W1 first -- the step-boundary bubble shrinks to W2's collective, which
+        # overlaps that first GEMM
+        self.swap0 = cfg.skip_input_grad
         for l in reversed(range(L)):
-            for name in ("w2", "w1"):
+            for name in self.layer_order(l):
                 fs = full[name]
                 own = (fs[0] // d, fs[1]) if self.fsdp else fs
                 e = Entry(l, name, own, fs, off)
@@ -202,11 +207,14 @@ class FFNTrainer:
                 goff += n
             self.ag_pending = [None] * len(self.buckets)
             self.rs_issued_at = [None] * len(self.buckets)
-            self.layer_buckets = {l: sorted({b for b, (s_, e_, _) in enumerate(self.buckets)
-                                             for n in ("w1", "w2")
-                                             if s_ < self.entry[(l, n)].offset + self.entry[(l, n)].numel
-                                             and self.entry[(l, n)].offset < e_})
-                                  for l in range(L)}
+            self.weight_buckets = {(l, n): sorted(b for b, (s_, e_, _) in enumerate(self.buckets)
+                                                  if s_ < self.entry[(l, n)].offset + self.entry[(l, n)].numel
+                                                  and self.entry[(l, n)].offset < e_)
+                                   for l in range(L) for n in ("w1", "w2")}
+            # the final buckets' optimizer + all-gather run on a side stream so the next step's first
+            # GEMM does not queue behind the last reduce-scatter (ordering: the forward waits for the
+            # all-gather, which was issued after the update on that stream)
+            self.opt_stream = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
             self._master_synced = True
         self._entry_index = {(e.layer, e.name): i for i, e in enumerate(self.entries)}
         self._next_bucket = 0
@@ -226,9 +234,13 @@ class FFNTrainer:
     def grad_view(self, l: int, name: str) -> torch.Tensor:
         return self._view(self.grads, self.entry[(l, name)])
 
+    def layer_order(self, l: int) -> tuple[str, str]:
+        """Order in which layer l's weight gradients complete in the backward (= flat layout order)."""
+        return ("w1", "w2") if (l == 0 and self.swap0) else ("w2", "w1")
+
     def _layer_range(self, l: int) -> tuple[int, int]:
-        e2, e1 = self.entry[(l, "w2")], self.entry[(l, "w1")]
-        return e2.offset, e1.offset + _round_up(e1.numel, self.align)
+        first, last = (self.entry[(l, n)] for n in self.layer_order(l))
+        return first.offset, last.offset + _round_up(last.numel, self.align)
 
     # ------------------------------------------------------------------------------------------------
     # parameters in / out (logical layout: per layer w1 [F,D], w2 [D,F] (+ w3 [F,D] if gated))
@@ -367,15 +379,21 @@ class FFNTrainer:
                 s, e, _ = self.buckets[b]
                 self.bucket_work[b] = comm.all_reduce(self.grads[s:e], self.mesh.group("dp_ar"), async_op=True)
                 self._next_bucket += 1
-        elif self.fsdp and name == "w1":
+        elif self.fsdp and name == self.layer_order(l)[1]:
             slot = l % 2
             g = self.gring[slot]
             works = [comm.reduce_scatter_into(self.grad_view(l, n), g[n], self.mesh.group("dp_rs"), async_op=True)
                      for n in ("w2", "w1")]
             self.rs_pending[slot] = (l, works)
 
-    def _zero_finish(self, b: int) -> None:
-        """Bucket b's reduce-scatter is done -> update the owned shard -> all-gather the new bf16 copy."""
+    def _zero_finish(self, b: int, side: bool = False) -> None:
+        """Bucket b's reduce-scatter is done -> update the owned shard -> all-gather the new bf16 copy.
+        ``side``: do it on ``opt_stream`` instead of the compute stream."""
+        if side and self.opt_stream is not None:
+            self.opt_stream.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self.opt_stream):
+                self._zero_finish(b)
+            return
         self.bucket_work[b].wait()
         self.bucket_work[b] = None
         s_, e_, _ = self.buckets[b]
@@ -457,18 +475,26 @@ class FFNTrainer:
                     self._fsdp_gather(l + 1)
             else:
                 if self.zero:
-                    for b in self.layer_buckets[l]:
+                    for b in self.weight_buckets[(l, "w1")]:
                         self._zero_wait_ag(b)
                 w1, w2 = self.copy_view(l, "w1"), self.copy_view(l, "w2")
             a = self.acts_a[l if keep else 0]
             h = (self.acts_h[l if keep else 0]) if self.need_h else None
             if self.sp:
+                if self.zero:
+                    for b in self.weight_buckets[(l, "w2")]:
+                        self._zero_wait_ag(b)
                 xin = self.xs_full[l] if keep else self.xfull
                 comm.all_gather_into(xin, self.xs[l], tpg, async_op=True).wait()
                 layer_fwd(xin, w1, w2, act, gated, a, h, self.yfull)
                 comm.reduce_scatter_into(self.xs[l + 1], self.yfull, tpg, async_op=True).wait()
             else:
-                layer_fwd(self.xs[l], w1, w2, act, gated, a, h, self.xs[l + 1])
+                before2 = None
+                if self.zero:
+                    def before2(l=l):
+                        for b in self.weight_buckets[(l, "w2")]:
+                            self._zero_wait_ag(b)
+                layer_fwd(self.xs[l], w1, w2, act, gated, a, h, self.xs[l + 1], before_fwd2=before2)
                 if self.mesh.tp > 1:
                     comm.all_reduce(self.xs[l + 1], tpg, async_op=True).wait()
         y = self.xs[L]
@@ -537,7 +563,7 @@ class FFNTrainer:
         if self.zero:
             for b, at in enumerate(self.rs_issued_at):
                 if at is not None:
-                    self._zero_finish(b)
+                    self._zero_finish(b, side=True)
         elif self.ddp:
             for b, (s, e, _) in enumerate(self.buckets):
                 self.bucket_work[b].wait()
