@@ -70,6 +70,8 @@ def parse():
                    help="gloo = CPU dry run of the multi-rank path (tests; tiny dims)")
     p.add_argument("--graph", action="store_true",
                    help="capture the whole step (data + fwd + bwd + fused SGD) in a HIP graph (N=1 path)")
+    p.add_argument("--lib_plain_nt", action="store_true",
+                   help="run the plain forward GEMM y = a·W2ᵀ (no epilogue) on hipBLASLt; all fused GEMMs stay native")
     p.add_argument("--force_comm", action="store_true",
                    help="exercise the RCCL DDP/FSDP path at N=1 (size-1 communicators, unfused optimizer)")
     return p.parse_args()
@@ -103,6 +105,10 @@ def main() -> int:
     else:
         tp = a.tp or min(n, 2)
         dp_mode, dp = "fsdp", n // tp
+    if a.lib_plain_nt:
+        from dllm.ops.gemm import set_library_plain_nt
+
+        set_library_plain_nt(True)
     m = ModelConfig(model_size=a.model_size, ffn_dim=a.ffn_dim, layers=a.layers, act=a.act, gated=a.gated)
     cfg = TrainConfig(model=m, batch_size=a.batch_size, seq_len=a.seq_len, num_steps=a.steps, dtype=a.dtype,
                       grad_dtype=a.grad_dtype, optimizer=a.optimizer, dp_mode=dp_mode, dp=dp, tp=tp,
@@ -167,6 +173,7 @@ def main() -> int:
                    "optimizer": a.optimizer, "grad_dtype": a.grad_dtype, "master_weights": "fp32"},
         "tflops_per_gpu": round(tflops, 1), "mfu_dense": round(tflops / PEAK_TFLOPS[a.dtype], 4),
         "peak_hbm_gib": round(peak_gib, 2), "finite": finite, "comm": a.comm, "hip_graph": bool(a.graph),
+        "plain_nt_gemm": "hipblaslt" if a.lib_plain_nt else "native",
     }
     if a.force_comm:
         rec["note"] = "force_comm: DDP/FSDP collectives over size-1 RCCL communicators"

@@ -61,7 +61,7 @@ def _headers_mtime() -> float:
     return m
 
 
-COMMON_FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-result"]
+COMMON_FLAGS = ["-O3", "-fPIC", "-std=c++20", f"--offload-arch={ARCH}", "-Wno-unused-result"]
 
 
 def _compile(src: str, verbose: bool) -> str:

@@ -158,6 +158,18 @@ def set_splitk(enabled: bool) -> bool:
     return old
 
 
+_LIBRARY_PLAIN_NT = {"enabled": False}
+
+
+def set_library_plain_nt(enabled: bool) -> bool:
+    """Route PLAIN NT GEMMs (store epilogue, alpha 1, beta 0, bf16 in and out — the forward ``y = a·W2ᵀ``)
+    to hipBLASLt through ``torch.matmul``.  Every fused GEMM (activation, mask, gate, optimizer) and every
+    NN/TN GEMM stays on the native kernels.  Returns the previous setting."""
+    old = _LIBRARY_PLAIN_NT["enabled"]
+    _LIBRARY_PLAIN_NT["enabled"] = bool(enabled)
+    return old
+
+
 def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None = None, *, epi: str = "store",
          act: str = "none", aux: torch.Tensor | None = None, aux_out: torch.Tensor | None = None,
          alpha: float = 1.0, beta: float = 0.0, out_dtype: torch.dtype | None = None, group_m: int = 4,
@@ -190,6 +202,9 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
 
     for t, nm in ((a, "a"), (b, "b"), (out, "out")):
         _check_rowmajor(t, nm)
+    if (_LIBRARY_PLAIN_NT["enabled"] and layout == "nt" and epi == "store" and alpha == 1.0 and beta == 0.0
+            and force is None and a.dtype == torch.bfloat16 and out.dtype == torch.bfloat16):
+        return torch.matmul(a, b.t(), out=out)
     auxt = aux if aux is not None else aux_out
     if auxt is not None:
         _check_rowmajor(auxt, "aux")
