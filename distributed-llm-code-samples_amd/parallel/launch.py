@@ -98,19 +98,25 @@ def run_rank(rank: int, world: int, cfg_dict: dict, method: int, backend: str, p
     seed_list = my_seeds.tolist()
     if start_step < len(seed_list):
         data.prefetch(int(seed_list[start_step]))
-    with maybe_profile(opts.get("profile", ""), rank):
-        for i, s in enumerate(seed_list):
-            if i < start_step:
-                continue
-            if i >= stop_after:
-                break
-            _maybe_inject_fault(rank, i)
-            timer.start()
-            nxt = seed_list[i + 1] if i + 1 < min(len(seed_list), stop_after) else None
-            x, dy = data.fill(int(s), next_seed=nxt)
-            eng.train_step(x, dy)
-            timer.stop()
-            done = i + 1
+    try:
+        with maybe_profile(opts.get("profile", ""), rank):
+            for i, s in enumerate(seed_list):
+                if i < start_step:
+                    continue
+                if i >= stop_after:
+                    break
+                _maybe_inject_fault(rank, i)
+                timer.start()
+                nxt = seed_list[i + 1] if i + 1 < min(len(seed_list), stop_after) else None
+                x, dy = data.fill(int(s), next_seed=nxt)
+                eng.train_step(x, dy)
+                timer.stop()
+                done = i + 1
+    except BaseException:
+        # error path: abort native communicators (no synchronising teardown against a dead peer) and
+        # let the parent see the failure; torch process groups time out / are torn down with the process
+        mesh.destroy(abort=True)
+        raise
     timer.finish()
     if opts.get("ckpt_dir"):
         save_checkpoint(eng, opts["ckpt_dir"], step=done, fmt=opts.get("ckpt_format", "consolidated"),

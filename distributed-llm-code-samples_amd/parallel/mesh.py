@@ -78,15 +78,20 @@ class Mesh:
     def group(self, role: str):
         return self.groups.get(role)
 
-    def destroy(self) -> None:
-        """Tear down native communicators (torch process groups are destroyed with the default PG)."""
+    def destroy(self, abort: bool = False) -> None:
+        """Tear down native communicators (torch process groups are destroyed with the default PG).
+        ``abort``: error path -- ``ncclCommAbort`` instead of a synchronising destroy, so a rank whose
+        peer died does not block in teardown."""
         from .rccl import NativeGroup
 
         seen = set()
         for g in self.groups.values():
             if isinstance(g, NativeGroup) and id(g) not in seen:
                 seen.add(id(g))
-                g.destroy()
+                if abort:
+                    g.abort()
+                else:
+                    g.destroy()
         self.groups.clear()
 
     @classmethod

@@ -175,6 +175,12 @@ class NativeGroup:
     def check_async_error(self) -> None:
         _check(_lib().dllm_nccl_comm_async_error(self.comm), "ncclCommGetAsyncError")
 
+    def abort(self) -> None:
+        """Error path: abort the communicator without waiting for outstanding work."""
+        if self.comm:
+            _lib().dllm_nccl_comm_abort(self.comm)
+            self.comm = None
+
     def destroy(self, abort: bool = False) -> None:
         if self.comm:
             torch.cuda.synchronize(self.device)

@@ -60,6 +60,25 @@ def test_native_work_orders_streams(pg):
     g.destroy()
 
 
+def test_native_abort_error_path(pg):
+    """ncclCommAbort path: a communicator with completed work aborts cleanly, and a mesh
+    torn down with abort=True leaves no communicator behind."""
+    from dllm.parallel.rccl import NativeGroup
+
+    dev = torch.device("cuda", 0)
+    g = NativeGroup([0], "abort", dev)
+    x = torch.ones(1024, device=dev)
+    g.all_reduce(x).wait()
+    torch.cuda.synchronize()
+    g.check_async_error()
+    g.abort()
+    assert g.comm is None
+    g.destroy()  # idempotent after abort (releases the stream)
+    mesh = Mesh.build(1, 1, force=True, comm_backend="native", device=dev)
+    mesh.destroy(abort=True)
+    assert not mesh.groups
+
+
 def _run(dp_mode, backend, dtype="fp32", opt="sgd", force=True):
     D, F, L, T = 256, 1024, 2, 512
     gen = torch.Generator().manual_seed(9)
