@@ -70,6 +70,9 @@ def parse():
                    help="gloo = CPU dry run of the multi-rank path (tests; tiny dims)")
     p.add_argument("--graph", action="store_true",
                    help="capture the whole step (data + fwd + bwd + fused SGD) in a HIP graph (N=1 path)")
+    p.add_argument("--side_opt", type=int, default=0,
+                   help="N=1: store wgrads and run SGD on a side stream over this many workgroups (0 = fuse the "
+                        "update into the wgrad GEMM epilogue)")
     p.add_argument("--lib_plain_nt", action="store_true",
                    help="run the plain forward GEMM y = a·W2ᵀ (no epilogue) on hipBLASLt; all fused GEMMs stay native")
     p.add_argument("--force_comm", action="store_true",
@@ -113,7 +116,7 @@ def main() -> int:
     cfg = TrainConfig(model=m, batch_size=a.batch_size, seq_len=a.seq_len, num_steps=a.steps, dtype=a.dtype,
                       grad_dtype=a.grad_dtype, optimizer=a.optimizer, dp_mode=dp_mode, dp=dp, tp=tp,
                       bucket_mb=a.bucket_mb, recompute=a.recompute, sequence_parallel=a.sequence_parallel,
-                      data="device", force_comm=a.force_comm, comm_backend=a.comm)
+                      data="device", force_comm=a.force_comm, comm_backend=a.comm, side_optimizer=a.side_opt)
     mesh = Mesh.build(dp, tp, force=a.force_comm, comm_backend="torch" if cpu else a.comm,
                       device=None if cpu else dev)
     eng = FFNTrainer(cfg, mesh, dev)

@@ -9,6 +9,8 @@
 // * dllm_cast         : fp32 <-> bf16.
 // All kernels: grid-stride, 4 elements per lane per iteration (16-B fp32 / 8-B bf16 accesses),
 // grid capped at 256 CUs x 8 blocks (cdna_hip_programming.md Guideline 11).
+#include <algorithm>
+
 #include "common.h"
 
 namespace dllm {
@@ -131,6 +133,40 @@ __global__ __launch_bounds__(256) void cast_bf16_f32_kernel(const uint16_t* in, 
     out[i] = bf2f(in[i]);
 }
 
+// Streaming SGD for a side stream that shares the GPU with compute-bound GEMMs: few workgroups
+// (max_blocks, e.g. 1/8 of the CUs), 512 threads, each thread keeping UNR f32x4 of master + grad in
+// flight so a handful of CUs still pull HBM bandwidth (~50 GB/s per CU at ~2 us latency).
+template <int UNR>
+__global__ __launch_bounds__(512) void sgd_stream_kernel(float* master, const void* grad, int gdt, uint16_t* copy,
+                                                         long n, float lr, float gscale) {
+  const long n4 = n / 4;
+  const long stride = (long)gridDim.x * blockDim.x;
+  long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  for (; i + (UNR - 1) * stride < n4; i += UNR * stride) {
+    f32x4_t p[UNR], g[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      p[u] = *(f32x4_t*)(master + 4 * (i + u * stride));
+      g[u] = load_grad4(grad, gdt, 4 * (i + u * stride));
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) p[u][j] = __fadd_rn(p[u][j], __fmul_rn(-lr, __fmul_rn(gscale, g[u][j])));
+      *(f32x4_t*)(master + 4 * (i + u * stride)) = p[u];
+      if (copy) store_bf16x4(copy, 4 * (i + u * stride), p[u]);
+    }
+  }
+  for (; i < n4; i += stride) {
+    f32x4_t p = *(f32x4_t*)(master + 4 * i);
+    const f32x4_t g = load_grad4(grad, gdt, 4 * i);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) p[j] = __fadd_rn(p[j], __fmul_rn(-lr, __fmul_rn(gscale, g[j])));
+    *(f32x4_t*)(master + 4 * i) = p;
+    if (copy) store_bf16x4(copy, 4 * i, p);
+  }
+}
+
 static inline int grid_for(long n4) {
   long g = (n4 + 255) / 256;
   if (g > 2048) g = 2048;
@@ -180,6 +216,17 @@ int dllm_sgd_step(float* master, const void* grad, int grad_dtype, void* copy_bf
                   void* stream) {
   if (n % 4) return -1;
   hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n / 4)), dim3(256), 0, (hipStream_t)stream, master, grad, grad_dtype,
+                     (uint16_t*)copy_bf16, n, lr, gscale);
+  return (int)hipGetLastError();
+}
+
+// same update as dllm_sgd_step, bitwise, on at most max_blocks workgroups (side-stream optimizer)
+int dllm_sgd_step_stream(float* master, const void* grad, int grad_dtype, void* copy_bf16, long n, float lr,
+                         float gscale, int max_blocks, void* stream) {
+  if (n % 4 || max_blocks <= 0) return -1;
+  const long n4 = n / 4;
+  const int g = (int)std::min<long>(max_blocks, std::max<long>(1, (n4 + 511) / 512));
+  hipLaunchKernelGGL(sgd_stream_kernel<8>, dim3(g), dim3(512), 0, (hipStream_t)stream, master, grad, grad_dtype,
                      (uint16_t*)copy_bf16, n, lr, gscale);
   return (int)hipGetLastError();
 }

@@ -90,15 +90,23 @@ def _grad_code(g: torch.Tensor) -> int:
 
 
 def sgd_step_(master: torch.Tensor, grad: torch.Tensor, lr: float, copy: torch.Tensor | None = None,
-              grad_scale: float = 1.0) -> None:
-    """``master += (-lr)·grad`` in place (reference ``param.add_(-LR*grad)``), then ``copy = bf16(master)``."""
+              grad_scale: float = 1.0, max_blocks: int = 0) -> None:
+    """``master += (-lr)·grad`` in place (reference ``param.add_(-LR*grad)``), then ``copy = bf16(master)``.
+    ``max_blocks > 0``: the streaming variant on at most that many workgroups (a side-stream optimizer
+    that leaves the rest of the GPU to concurrent GEMMs); bitwise the same update."""
     if master.dtype != torch.float32:
         raise TypeError("master weights must be fp32")
     if master.device.type == "cuda":
         n = master.numel()
         if n % 4 == 0 and master.is_contiguous() and grad.is_contiguous():
-            rc = _native.lib().dllm_sgd_step(master.data_ptr(), grad.data_ptr(), _grad_code(grad),
-                                             copy.data_ptr() if copy is not None else None, n, float(lr),
+            cp = copy.data_ptr() if copy is not None else None
+            if max_blocks > 0:
+                rc = _native.lib().dllm_sgd_step_stream(master.data_ptr(), grad.data_ptr(), _grad_code(grad), cp, n,
+                                                        float(lr), float(grad_scale), int(max_blocks),
+                                                        _native.stream_ptr(master.device))
+                _native.check(rc, "dllm_sgd_step_stream")
+                return
+            rc = _native.lib().dllm_sgd_step(master.data_ptr(), grad.data_ptr(), _grad_code(grad), cp, n, float(lr),
                                              float(grad_scale), _native.stream_ptr(master.device))
             _native.check(rc, "dllm_sgd_step")
             return

@@ -150,8 +150,15 @@ class FFNTrainer:
         self.copy = self.master if self.shared_copy else torch.zeros(self.total, dtype=self.cd, device=dev)
         # no gradient collective (single device / pure TP): the optimizer runs inside the wgrad GEMMs and
         # no flat gradient buffer exists at all
-        self.fused_opt = cfg.fused_optimizer and not (self.ddp or self.fsdp or self.zero)
+        no_coll = not (self.ddp or self.fsdp or self.zero)
+        # side-stream optimizer: wgrad GEMMs store the gradient, a low-occupancy SGD kernel on its own
+        # stream updates the weight while the next GEMMs run; the forward waits per weight
+        self.side_opt = (no_coll and cfg.side_optimizer > 0 and cfg.optimizer == "sgd" and dev.type == "cuda")
+        self.fused_opt = cfg.fused_optimizer and no_coll and not self.side_opt
         self.grads = torch.zeros(0 if self.fused_opt else self.total, dtype=self.gd, device=dev)
+        if self.side_opt:
+            self.opt_stream_side = torch.cuda.Stream(device=dev)
+            self.opt_done = {}
         if cfg.optimizer == "adam":
             self.adam_m = torch.zeros(self.total, dtype=torch.float32, device=dev)
             self.adam_v = torch.zeros(self.total, dtype=torch.float32, device=dev)
@@ -259,6 +266,7 @@ class FFNTrainer:
         owned shards are all-gathered first so every buffer is complete on every rank (collective)."""
         if self.zero:
             self.zero_sync_state()
+        self.side_sync()
         out = {"params": self.master}
         if self.cfg.optimizer == "adam":
             out["adam_m"], out["adam_v"] = self.adam_m, self.adam_v
@@ -302,6 +310,7 @@ class FFNTrainer:
     def local_params(self, flat: torch.Tensor | None = None) -> list[dict]:
         """This TP rank's full local (unsharded over dp) fp32 tensors of a flat buffer, w1 de-interleaved.
         Collective over the dp group under FSDP."""
+        self.side_sync()
         src = self.master if flat is None else flat
         out = []
         for l in range(self.L):
@@ -362,6 +371,19 @@ class FFNTrainer:
     # communication hooks
     # ------------------------------------------------------------------------------------------------
     def _grad_ready(self, l: int, name: str) -> None:
+        if self.side_opt:
+            e = self.entry[(l, name)]
+            s_, e_ = e.offset, e.offset + e.numel
+            st = self.opt_stream_side
+            st.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(st):
+                copy = None if self.shared_copy else self.copy[s_:e_]
+                sgd_step_(self.master[s_:e_], self.grads[s_:e_], self.cfg.lr, copy=copy,
+                          max_blocks=self.cfg.side_optimizer)
+                ev = torch.cuda.Event()
+                ev.record(st)
+            self.opt_done[(l, name)] = ev
+            return
         if self.zero:
             idx = self._entry_index[(l, name)]
             while self._next_bucket < len(self.buckets) and self.buckets[self._next_bucket][2] <= idx:
@@ -411,6 +433,17 @@ class FFNTrainer:
             src = src.clone()  # gloo: keep input and output of the all-gather disjoint
         self.ag_pending[b] = comm.all_gather_into(self.copy[s_:e_], src, self.mesh.group("dp_ag"), async_op=True)
         self.rs_issued_at[b] = None
+
+    def _side_wait(self, l: int, name: str) -> None:
+        ev = self.opt_done.pop((l, name), None)
+        if ev is not None:
+            torch.cuda.current_stream(self.device).wait_event(ev)
+
+    def side_sync(self) -> None:
+        """Make the current stream wait for every pending side-stream update (checkpoint / readout)."""
+        if self.side_opt:
+            for k in list(self.opt_done):
+                self._side_wait(*k)
 
     def _zero_wait_ag(self, b: int) -> None:
         if self.ag_pending[b] is not None:
@@ -477,6 +510,8 @@ class FFNTrainer:
                 if self.zero:
                     for b in self.weight_buckets[(l, "w1")]:
                         self._zero_wait_ag(b)
+                if self.side_opt:
+                    self._side_wait(l, "w1")
                 w1, w2 = self.copy_view(l, "w1"), self.copy_view(l, "w2")
             a = self.acts_a[l if keep else 0]
             h = (self.acts_h[l if keep else 0]) if self.need_h else None
@@ -484,6 +519,8 @@ class FFNTrainer:
                 if self.zero:
                     for b in self.weight_buckets[(l, "w2")]:
                         self._zero_wait_ag(b)
+                if self.side_opt:
+                    self._side_wait(l, "w2")
                 xin = self.xs_full[l] if keep else self.xfull
                 comm.all_gather_into(xin, self.xs[l], tpg, async_op=True).wait()
                 layer_fwd(xin, w1, w2, act, gated, a, h, self.yfull)
@@ -494,6 +531,9 @@ class FFNTrainer:
                     def before2(l=l):
                         for b in self.weight_buckets[(l, "w2")]:
                             self._zero_wait_ag(b)
+                elif self.side_opt:
+                    def before2(l=l):
+                        self._side_wait(l, "w2")
                 layer_fwd(self.xs[l], w1, w2, act, gated, a, h, self.xs[l + 1], before_fwd2=before2)
                 if self.mesh.tp > 1:
                     comm.all_reduce(self.xs[l + 1], tpg, async_op=True).wait()
@@ -571,7 +611,7 @@ class FFNTrainer:
         elif self.fsdp:
             for slot in ((L - 1) % 2, L % 2):
                 self._fsdp_finish_rs(slot)
-        elif not self.fused_opt:
+        elif not self.fused_opt and not self.side_opt:
             self._opt(0, self.total)
         return y
 

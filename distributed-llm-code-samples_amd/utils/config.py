@@ -65,6 +65,8 @@ class TrainConfig:
     separate_streams: bool = True    # one communicator/stream per comm role
     tp_overlap: bool = True          # overlap the TP dx all-reduce with the dW1 GEMM
     fused_optimizer: bool = True     # fuse SGD/Adam into the wgrad GEMM epilogue when no grad collective
+    side_optimizer: int = 0          # >0 (no grad collective, SGD): wgrad GEMMs store grads and a side stream
+                                     # applies SGD on this many workgroups, overlapped with the next GEMMs
     force_comm: bool = False         # run the DDP/FSDP collective path even at dp=1 (single-GPU RCCL check)
     comm_backend: str = "torch"      # torch (ProcessGroupNCCL/gloo) | native (csrc/comm.cpp RCCL layer)
     debug_sync: bool = False         # race screen: wait every collective at issue + device sync per layer
