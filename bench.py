@@ -63,6 +63,10 @@ def parse():
     p.add_argument("--recompute", default="none")
     p.add_argument("--sequence_parallel", action="store_true")
     p.add_argument("--seed", type=int, default=1234)
+    p.add_argument("--init_scale", default="auto",
+                   help="weight init std: a number, 'fan_in' (1/sqrt(fan_in) per matrix), or 'auto' = the "
+                        "reference's 2e-2 for plain FFN stacks and fan_in for gated (SwiGLU) stacks, which "
+                        "overflow with 2e-2 once deep (no norms/residuals in this model)")
     p.add_argument("--json_out", default="")
     p.add_argument("--comm", choices=["torch", "native"], default="torch",
                    help="role communicators: torch ProcessGroupNCCL or the native C++ RCCL layer")
@@ -122,7 +126,9 @@ def main() -> int:
     eng = FFNTrainer(cfg, mesh, dev)
     from dllm.models.ffn import init_ffn_params_device
 
-    eng.load_full_params(init_ffn_params_device(m.D, m.F, m.layers, a.seed, dev, m.gated))
+    init_scale = ("fan_in" if m.gated else 2e-2) if a.init_scale == "auto" else (
+        a.init_scale if a.init_scale == "fan_in" else float(a.init_scale))
+    eng.load_full_params(init_ffn_params_device(m.D, m.F, m.layers, a.seed, dev, m.gated, scale=init_scale))
     sync()
     data = DeviceMockData(cfg.tokens, m.D, cfg.torch_dtype, dev)
     seed_base = 10_000 * (mesh.dp_rank + 1)
@@ -173,7 +179,8 @@ def main() -> int:
         "data": "synthetic (device Philox N(0,1) x, 0.1*N(0,1) dloss/dx; random-init weights)",
         "config": {"model": f"ffn-stack L{m.layers} D{m.D} F{m.F} {'swiglu-' if m.gated else ''}{m.act}",
                    "global_batch": a.batch_size * dp, "seq_len": a.seq_len, "parallelism": par,
-                   "optimizer": a.optimizer, "grad_dtype": a.grad_dtype, "master_weights": "fp32"},
+                   "optimizer": a.optimizer, "grad_dtype": a.grad_dtype, "master_weights": "fp32",
+                   "init_scale": init_scale},
         "tflops_per_gpu": round(tflops, 1), "mfu_dense": round(tflops / PEAK_TFLOPS[a.dtype], 4),
         "peak_hbm_gib": round(peak_gib, 2), "finite": finite, "comm": a.comm, "hip_graph": bool(a.graph),
         "plain_nt_gemm": "hipblaslt" if a.lib_plain_nt else "native",
