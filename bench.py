@@ -77,6 +77,9 @@ def parse():
     p.add_argument("--side_opt", type=int, default=0,
                    help="N=1: store wgrads and run SGD on a side stream over this many workgroups (0 = fuse the "
                         "update into the wgrad GEMM epilogue)")
+    p.add_argument("--gemm_variant", default="auto",
+                   choices=["auto", "2stage", "8phase", "8phase_stagger", "4phase_stagger"],
+                   help="bf16 GEMM main-loop schedule (auto = 4-phase staggered when K % 128 == 0)")
     p.add_argument("--lib_plain_nt", action="store_true",
                    help="run the plain forward GEMM y = a·W2ᵀ (no epilogue) on hipBLASLt; all fused GEMMs stay native")
     p.add_argument("--force_comm", action="store_true",
@@ -112,6 +115,10 @@ def main() -> int:
     else:
         tp = a.tp or min(n, 2)
         dp_mode, dp = "fsdp", n // tp
+    if a.gemm_variant != "auto" and not cpu:
+        from dllm.ops.gemm import set_bf16_variant
+
+        set_bf16_variant(a.gemm_variant)
     if a.lib_plain_nt:
         from dllm.ops.gemm import set_library_plain_nt
 
@@ -183,7 +190,7 @@ def main() -> int:
                    "init_scale": init_scale},
         "tflops_per_gpu": round(tflops, 1), "mfu_dense": round(tflops / PEAK_TFLOPS[a.dtype], 4),
         "peak_hbm_gib": round(peak_gib, 2), "finite": finite, "comm": a.comm, "hip_graph": bool(a.graph),
-        "plain_nt_gemm": "hipblaslt" if a.lib_plain_nt else "native",
+        "plain_nt_gemm": "hipblaslt" if a.lib_plain_nt else "native", "gemm_variant": a.gemm_variant,
     }
     if a.force_comm:
         rec["note"] = "force_comm: DDP/FSDP collectives over size-1 RCCL communicators"

@@ -681,7 +681,10 @@ __device__ __forceinline__ bf16x8_t cat_tr(s16x4_t lo, s16x4_t hi) {
 // K-contiguous fragment READS of A/B, independent of LAYOUT (wrong results, same work) -- isolates the
 // cost of MN-contiguous LDS-DMA patterns vs transposed ds_read_b64_tr_b16 fragment reads.
 // ACT >= 0: activation of the ACT/DACT/GLU/DGLU epilogues fixed at compile time (-1: runtime p.act)
-template <int LAYOUT, int EPI, typename OutT, bool STAGGER, int ABL = 0, int ACT = -1>
+// NPH = 8: the 8-phase schedule below (one quadrant = 16 MFMAs per wave per barrier interval).
+// NPH = 4: half-tile phases (two quadrants = 32 MFMAs per interval, two half-tiles restaged per phase):
+// halves the barrier count per MFMA (see the NPH == 4 loop).
+template <int LAYOUT, int EPI, typename OutT, bool STAGGER, int ABL = 0, int ACT = -1, int NPH = 8>
 __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
   // slot(op, hh, buf) = ((op*2 + hh)*2 + buf) * 16 KiB: A in [0, 64K), B in [64K, 128K), so every
   // fragment read is base + a 16-bit immediate
@@ -763,7 +766,7 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
 
   bf16x8_t fa[4][2], fb0[2][2], fb1[2][2];  // [tile][k-substep]
   // transposed-read halves: issued in the read segment, combined after the phase's single lgkmcnt(0)
-  s16x4_t ta_lo[4][2], ta_hi[4][2], tb_lo[2][2], tb_hi[2][2];
+  s16x4_t ta_lo[4][2], ta_hi[4][2], tb_lo[2][2], tb_hi[2][2], tc_lo[2][2], tc_hi[2][2];
 
   // A half hh of buffer buf -> fa ; B half hh of buffer buf -> fb   (issue only)
   auto read_a = [&](auto hh_c, auto buf_c) {
@@ -810,6 +813,26 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) fb[t][s2] = cat_tr(tb_lo[t][s2], tb_hi[t][s2]);
     }
+  };  // second B half in the same phase (NPH == 4): its own transposed-read temporaries
+  auto read_b2 = [&](auto hh_c, auto buf_c, bf16x8_t (&fb)[2][2]) {
+    constexpr int SO = (hh_c.value * 2 + buf_c.value) * HT;
+    if constexpr (B_RKC) {
+      lds_b128<SO + 0 * 2048>(fb[0][0], bbase[0]); lds_b128<SO + 1 * 2048>(fb[1][0], bbase[0]);
+      lds_b128<SO + 0 * 2048>(fb[0][1], bbase[1]); lds_b128<SO + 1 * 2048>(fb[1][1], bbase[1]);
+    } else {
+#define DLLM_TRC(t, s)                                              \
+  lds_tr16<SO + (s) * 8192>(tc_lo[t][s], bbase[t]);                 \
+  lds_tr16<SO + (s) * 8192 + 1024>(tc_hi[t][s], bbase[t]);
+      DLLM_TRC(0, 0) DLLM_TRC(1, 0) DLLM_TRC(0, 1) DLLM_TRC(1, 1)
+#undef DLLM_TRC
+    }
+  };  auto fin_b2 = [&](bf16x8_t (&fb)[2][2]) {
+    if constexpr (!B_RKC) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) fb[t][s2] = cat_tr(tc_lo[t][s2], tc_hi[t][s2]);
+    }
   };
   auto mfma_quad = [&](f32x4_t (&c)[4][2], const bf16x8_t (&fb)[2][2]) {
     __builtin_amdgcn_s_setprio(1);
@@ -825,6 +848,54 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
 
+  if constexpr (NPH == 4) {
+    // Half-tile phases: P0 (tile te: quadrants (0,0),(0,1); reads A0 B0 B1), P1 (te: (1,1),(1,0); reads
+    // A1), P2 / P3 the same on tile to.  Two half-tiles restaged per phase, each >= 1 phase after its
+    // last read (lgkmcnt(0) before the reading phase's first barrier):
+    //   P0 B1o A1o (tile to)   P1 A0e B0e (te+2)   P2 B1e A1e (te+2)   P3 A0o B0o (to+2)
+    // vmcnt before each phase's first barrier retires exactly what the next phase reads:
+    //   P0 -> A1e: 8 pieces younger (A0o B0o B1o A1o)   P1 -> A0o B0o B1o: 6 younger
+    //   P2 -> A1o: 8 younger                             P3 -> A0e' B0e' B1e': 6 younger
+    stage(0, 0, 0, 0); stage(1, 0, 0, 0); stage(1, 1, 0, 0); stage(0, 1, 0, 0);
+    stage(0, 0, 1, 1); stage(1, 0, 1, 1);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    DLLM_BARRIER();
+    if constexpr (STAGGER) {
+      if (wr == 1) DLLM_BARRIER();
+    }
+    for (int it = 0; it < nk / 2; ++it) {
+      const int te = 2 * it, to = 2 * it + 1;
+#define DLLM_PHASE_END4(N)                                            \
+  asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory");               \
+  DLLM_LDS_WAIT();                                                    \
+  DLLM_BARRIER();
+      read_a(I0{}, I0{}); read_b(I0{}, I0{}, fb0); read_b2(I1{}, I0{}, fb1);
+      stage(1, 1, to, 1); stage(0, 1, to, 1);            // P0: B1 A1 odd
+      DLLM_PHASE_END4(8)
+      fin_a(); fin_b(fb0); fin_b2(fb1);
+      mfma_quad(acc[0][0], fb0); mfma_quad(acc[0][1], fb1);
+      DLLM_BARRIER();
+      read_a(I1{}, I0{});
+      stage(0, 0, te + 2, 0); stage(1, 0, te + 2, 0);    // P1: A0 B0 even
+      DLLM_PHASE_END4(6)
+      fin_a();
+      mfma_quad(acc[1][1], fb1); mfma_quad(acc[1][0], fb0);
+      DLLM_BARRIER();
+      read_a(I0{}, I1{}); read_b(I0{}, I1{}, fb0); read_b2(I1{}, I1{}, fb1);
+      stage(1, 1, te + 2, 0); stage(0, 1, te + 2, 0);    // P2: B1 A1 even
+      DLLM_PHASE_END4(8)
+      fin_a(); fin_b(fb0); fin_b2(fb1);
+      mfma_quad(acc[0][0], fb0); mfma_quad(acc[0][1], fb1);
+      DLLM_BARRIER();
+      read_a(I1{}, I1{});
+      stage(0, 0, to + 2, 1); stage(1, 0, to + 2, 1);    // P3: A0 B0 odd
+      DLLM_PHASE_END4(6)
+      fin_a();
+      mfma_quad(acc[1][1], fb1); mfma_quad(acc[1][0], fb0);
+      DLLM_BARRIER();
+#undef DLLM_PHASE_END4
+    }
+  } else {
   // prologue: tile 0 -> even buffer (4 half-tiles), tile 1 -> odd (A0, B0, B1; A1 comes at P0)
   stage(0, 0, 0, 0); stage(1, 0, 0, 0); stage(1, 1, 0, 0); stage(0, 1, 0, 0);
   stage(0, 0, 1, 1); stage(1, 0, 1, 1); stage(1, 1, 1, 1);
@@ -888,6 +959,7 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
     DLLM_BARRIER();
 #undef DLLM_PHASE_END
   }
+  }  // NPH == 8
   if constexpr (STAGGER) {
     if (wr == 0) DLLM_BARRIER();
   }
@@ -1133,6 +1205,10 @@ __global__ __launch_bounds__(256) void splitk_reduce(GemmArgs p, const float* ws
   }
 }
 
+// variant: 0 = auto (8-phase staggered when K % 128 == 0, else 2-stage), 1 = 2-stage, 2 = 8-phase, 3 = 8-phase staggered,
+// 4 = 4-phase (half-tile phases) staggered
+static int g_bf16_variant = 0;
+
 // main kernel writes partials into the workspace, then the reduction applies the epilogue
 template <int L, int E>
 static hipError_t launch_splitk(const GemmArgs& a, int out_dt, float* ws, hipStream_t s) {
@@ -1142,7 +1218,8 @@ static hipError_t launch_splitk(const GemmArgs& a, int out_dt, float* ws, hipStr
   w.alpha = 1.f;
   w.beta = 0.f;
   const int nb = (a.M / BT_M) * (a.N / BT_N) * a.ksplit;
-  hipLaunchKernelGGL((gemm_bf16_8ph<L, EPI_STORE, float, true>), dim3(nb), dim3(512), 0, s, w);
+  if (g_bf16_variant == 4) hipLaunchKernelGGL((gemm_bf16_8ph<L, EPI_STORE, float, true, 0, -1, 4>), dim3(nb), dim3(512), 0, s, w);
+  else hipLaunchKernelGGL((gemm_bf16_8ph<L, EPI_STORE, float, true>), dim3(nb), dim3(512), 0, s, w);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   long n4 = (long)a.M * (a.N / 4);
@@ -1155,26 +1232,24 @@ static hipError_t launch_splitk(const GemmArgs& a, int out_dt, float* ws, hipStr
 // ----------------------------------------------------------------------------------------------
 // host dispatch
 // ----------------------------------------------------------------------------------------------
-// variant: 0 = auto (8-phase when K % 128 == 0, else 2-stage), 1 = 2-stage, 2 = 8-phase, 3 = 8-phase staggered
-static int g_bf16_variant = 0;
 
 static float* g_splitk_ws = nullptr;  // set per call by dllm_gemm (caller-owned workspace)
 
 // staggered 8-phase launch; the FFN's own activation epilogues (NT act/glu forward, NN dact/dglu
 // dgrad, bf16 out) get a compile-time activation, everything else the runtime switch
-template <int L, int E, typename OutT>
+template <int L, int E, typename OutT, int NPH>
 static void launch_8ph_stagger(const GemmArgs& a, int nb, hipStream_t s) {
   constexpr bool fwd = L == L_NT && (E == EPI_ACT || E == EPI_GLU);
   constexpr bool bwd = L == L_NN && (E == EPI_DACT || E == EPI_DGLU);
   if constexpr ((fwd || bwd) && std::is_same<OutT, uint16_t>::value) {
     switch (a.act) {
-      case ACT_RELU: hipLaunchKernelGGL((gemm_bf16_8ph<L, E, OutT, true, 0, ACT_RELU>), dim3(nb), dim3(512), 0, s, a); return;
-      case ACT_SILU: hipLaunchKernelGGL((gemm_bf16_8ph<L, E, OutT, true, 0, ACT_SILU>), dim3(nb), dim3(512), 0, s, a); return;
-      case ACT_GELU: hipLaunchKernelGGL((gemm_bf16_8ph<L, E, OutT, true, 0, ACT_GELU>), dim3(nb), dim3(512), 0, s, a); return;
+      case ACT_RELU: hipLaunchKernelGGL((gemm_bf16_8ph<L, E, OutT, true, 0, ACT_RELU, NPH>), dim3(nb), dim3(512), 0, s, a); return;
+      case ACT_SILU: hipLaunchKernelGGL((gemm_bf16_8ph<L, E, OutT, true, 0, ACT_SILU, NPH>), dim3(nb), dim3(512), 0, s, a); return;
+      case ACT_GELU: hipLaunchKernelGGL((gemm_bf16_8ph<L, E, OutT, true, 0, ACT_GELU, NPH>), dim3(nb), dim3(512), 0, s, a); return;
       default: break;
     }
   }
-  hipLaunchKernelGGL((gemm_bf16_8ph<L, E, OutT, true>), dim3(nb), dim3(512), 0, s, a);
+  hipLaunchKernelGGL((gemm_bf16_8ph<L, E, OutT, true, 0, -1, NPH>), dim3(nb), dim3(512), 0, s, a);
 }
 
 template <int L, int E>
@@ -1191,9 +1266,12 @@ static hipError_t launch_bf16(const GemmArgs& a, int out_dt, hipStream_t s) {
   } else if (v == 2) {
     if (f32) hipLaunchKernelGGL((gemm_bf16_8ph<L, E, float, false>), dim3(nb), dim3(512), 0, s, a);
     else hipLaunchKernelGGL((gemm_bf16_8ph<L, E, uint16_t, false>), dim3(nb), dim3(512), 0, s, a);
+  } else if (v == 4) {
+    if (f32) launch_8ph_stagger<L, E, float, 4>(a, nb, s);
+    else launch_8ph_stagger<L, E, uint16_t, 4>(a, nb, s);
   } else {
-    if (f32) launch_8ph_stagger<L, E, float>(a, nb, s);
-    else launch_8ph_stagger<L, E, uint16_t>(a, nb, s);
+    if (f32) launch_8ph_stagger<L, E, float, 8>(a, nb, s);
+    else launch_8ph_stagger<L, E, uint16_t, 8>(a, nb, s);
   }
   return hipGetLastError();
 }
@@ -1241,7 +1319,9 @@ static hipError_t dispatch_opt(int path, const GemmArgs& a, int in_dt, hipStream
   if (path == 0 && a.ksplit > 1) return launch_splitk<L_TN, E>(a, DT_F32, g_splitk_ws, s);
   if (path == 0) {
     const int nb = (a.M / BT_M) * (a.N / BT_N);
-    if (a.K % (2 * BT_K) == 0 && g_bf16_variant != 1)
+    if (a.K % (2 * BT_K) == 0 && g_bf16_variant == 4)
+      hipLaunchKernelGGL((gemm_bf16_8ph<L_TN, E, float, true, 0, -1, 4>), dim3(nb), dim3(512), 0, s, a);
+    else if (a.K % (2 * BT_K) == 0 && g_bf16_variant != 1)
       hipLaunchKernelGGL((gemm_bf16_8ph<L_TN, E, float, true>), dim3(nb), dim3(512), 0, s, a);
     else
       hipLaunchKernelGGL((gemm_bf16_256<L_TN, E, float>), dim3(nb), dim3(512), 0, s, a);

@@ -236,7 +236,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
     return out
 
 
-BF16_VARIANTS = {"auto": 0, "2stage": 1, "8phase": 2, "8phase_stagger": 3}
+BF16_VARIANTS = {"auto": 0, "2stage": 1, "8phase": 2, "8phase_stagger": 3, "4phase_stagger": 4}
 
 
 def set_bf16_variant(name: str) -> str:

@@ -39,7 +39,7 @@ def _ref(a, b, layout):
     return {"nt": lambda: a @ b.t(), "nn": lambda: a @ b, "tn": lambda: a.t() @ b}[layout]()
 
 
-@pytest.fixture(params=["2stage", "8phase", "8phase_stagger"])
+@pytest.fixture(params=["2stage", "8phase", "8phase_stagger", "4phase_stagger"])
 def variant(request):
     old = set_bf16_variant(request.param)
     yield request.param
