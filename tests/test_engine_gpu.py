@@ -150,3 +150,27 @@ def test_fused_optimizer_epilogue_matches_separate_kernel(opt, dtype):
     for g, w in zip(*out):
         for k in w:
             torch.testing.assert_close(g[k], w[k], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_odd_shapes_and_skipped_input_grad(dtype):
+    """Shapes off every MFMA tile grid (generic kernel end to end) with the default skipped layer-0 input
+    gradient (layer 0 runs dW1 before dW2; the flat layout follows) against the oracle."""
+    D, F, L, T, lr = 96, 384, 3, 200, 1e-2
+    layers, batches = _setup(D, F, L, T, "relu", False, 2)
+    cfg = TrainConfig(model=ModelConfig(D, F, L), batch_size=1, seq_len=T, dtype=dtype, grad_dtype="fp32", lr=lr)
+    assert cfg.skip_input_grad
+    eng = FFNTrainer(cfg, Mesh(), torch.device("cuda"))
+    assert eng.layer_order(0) == ("w1", "w2") and eng.layer_order(1) == ("w2", "w1")
+    eng.load_full_params(layers)
+    cd = torch.float32 if dtype == "fp32" else torch.bfloat16
+    for x, dy in batches:
+        eng.train_step(x.cuda().to(cd), dy.cuda().to(cd))
+    got = eng.gather_full_params()
+    want = (R.train_single(layers, batches, lr) if dtype == "fp32"
+            else R.train_single_mixed(layers, batches, lr))
+    for g, w, p0 in zip(got, want, layers):
+        for k in g:
+            d_got, d_want = g[k].double() - p0[k].double(), w[k].double() - p0[k].double()
+            rel = (d_got - d_want).norm() / d_want.norm()
+            assert rel < (2e-3 if dtype == "fp32" else 2e-2), (k, rel.item())
