@@ -77,6 +77,8 @@ def parse():
     p.add_argument("--side_opt", type=int, default=0,
                    help="N=1: store wgrads and run SGD on a side stream over this many workgroups (0 = fuse the "
                         "update into the wgrad GEMM epilogue)")
+    p.add_argument("--tp_allreduce", choices=["rccl", "custom"], default="rccl",
+                   help="TP activation all-reduce: RCCL, or the custom two-shot xGMI peer all-reduce (csrc/car.hip)")
     p.add_argument("--gemm_variant", default="auto",
                    choices=["auto", "2stage", "8phase", "8phase_stagger", "4phase_stagger"],
                    help="bf16 GEMM main-loop schedule (auto = 4-phase staggered when K % 128 == 0)")
@@ -127,7 +129,7 @@ def main() -> int:
     cfg = TrainConfig(model=m, batch_size=a.batch_size, seq_len=a.seq_len, num_steps=a.steps, dtype=a.dtype,
                       grad_dtype=a.grad_dtype, optimizer=a.optimizer, dp_mode=dp_mode, dp=dp, tp=tp,
                       bucket_mb=a.bucket_mb, recompute=a.recompute, sequence_parallel=a.sequence_parallel,
-                      data="device", force_comm=a.force_comm, comm_backend=a.comm, side_optimizer=a.side_opt)
+                      data="device", force_comm=a.force_comm, comm_backend=a.comm, side_optimizer=a.side_opt, tp_allreduce=a.tp_allreduce)
     mesh = Mesh.build(dp, tp, force=a.force_comm, comm_backend="torch" if cpu else a.comm,
                       device=None if cpu else dev)
     eng = FFNTrainer(cfg, mesh, dev)
@@ -191,6 +193,7 @@ def main() -> int:
         "tflops_per_gpu": round(tflops, 1), "mfu_dense": round(tflops / PEAK_TFLOPS[a.dtype], 4),
         "peak_hbm_gib": round(peak_gib, 2), "finite": finite, "comm": a.comm, "hip_graph": bool(a.graph),
         "plain_nt_gemm": "hipblaslt" if a.lib_plain_nt else "native", "gemm_variant": a.gemm_variant,
+        "tp_allreduce": a.tp_allreduce,
     }
     if a.force_comm:
         rec["note"] = "force_comm: DDP/FSDP collectives over size-1 RCCL communicators"

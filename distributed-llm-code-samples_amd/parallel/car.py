@@ -104,6 +104,28 @@ class CustomAllReduce:
                       "dllm_car_all_reduce")
         return _Done()
 
+    def all_reduce_async(self, t: torch.Tensor):
+        """Enqueue on this object's own stream behind the current stream; ``wait()`` makes the current
+        stream wait for the result (the TP dx all-reduce overlapping the dW1 GEMM)."""
+        cur = torch.cuda.current_stream(self.device)
+        if getattr(self, "_stream", None) is None:
+            self._stream = torch.cuda.Stream(device=self.device)
+        self._stream.wait_stream(cur)
+        self.all_reduce(t, stream=self._stream)
+        ev = torch.cuda.Event()
+        ev.record(self._stream)
+        t.record_stream(self._stream)
+
+        class _Work:
+            def wait(_self):
+                torch.cuda.current_stream(self.device).wait_event(ev)
+                return True
+
+            def is_completed(_self):
+                return ev.query()
+
+        return _Work()
+
     def check(self) -> None:
         """Raise if a barrier timed out (synchronises the device first)."""
         torch.cuda.synchronize(self.device)

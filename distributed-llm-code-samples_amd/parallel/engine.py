@@ -79,7 +79,10 @@ class _Hooks:
     def after_dx(self, dx):
         e = self.eng
         if e.mesh.tp > 1:
-            self.tp_work = comm.all_reduce(dx, e.mesh.group("tp"), async_op=True)
+            if e.tp_car is not None:
+                self.tp_work = e.tp_car.all_reduce_async(dx)
+            else:
+                self.tp_work = comm.all_reduce(dx, e.mesh.group("tp"), async_op=True)
             if not e.cfg.tp_overlap:
                 self.tp_work.wait()
                 self.tp_work = None
@@ -124,6 +127,14 @@ class FFNTrainer:
         dev = self.device
         if cfg.debug_sync:
             comm.set_serialize(True)
+        # custom xGMI all-reduce for the TP activation exchange (opt-in; gradients stay on RCCL)
+        self.tp_car = None
+        if cfg.tp_allreduce == "custom" and t > 1 and self.device.type == "cuda" and not cfg.sequence_parallel:
+            from .car import CustomAllReduce
+
+            self.tp_car = CustomAllReduce(mesh.tp_ranks, self.device, cap_bytes=cfg.tokens * D * 4,
+                                          tag=f"tp{mesh.dp_rank}")
+            mesh.groups["tp_car"] = self.tp_car
 
         # ---- flat owned parameter layout (completion order) ------------------------------------
         full = {"w2": (D, self.F_loc), "w1": (self.R1, D)}
@@ -535,7 +546,9 @@ class FFNTrainer:
                     def before2(l=l):
                         self._side_wait(l, "w2")
                 layer_fwd(self.xs[l], w1, w2, act, gated, a, h, self.xs[l + 1], before_fwd2=before2)
-                if self.mesh.tp > 1:
+                if self.tp_car is not None:
+                    self.tp_car.all_reduce(self.xs[l + 1])
+                elif self.mesh.tp > 1:
                     comm.all_reduce(self.xs[l + 1], tpg, async_op=True).wait()
         y = self.xs[L]
 

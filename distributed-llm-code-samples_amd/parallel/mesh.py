@@ -82,10 +82,15 @@ class Mesh:
         """Tear down native communicators (torch process groups are destroyed with the default PG).
         ``abort``: error path -- ``ncclCommAbort`` instead of a synchronising destroy, so a rank whose
         peer died does not block in teardown."""
+        from .car import CustomAllReduce
         from .rccl import NativeGroup
 
         seen = set()
         for g in self.groups.values():
+            if isinstance(g, CustomAllReduce) and id(g) not in seen:
+                seen.add(id(g))
+                g.destroy()
+                continue
             if isinstance(g, NativeGroup) and id(g) not in seen:
                 seen.add(id(g))
                 if abort:

@@ -69,6 +69,7 @@ class TrainConfig:
                                      # applies SGD on this many workgroups, overlapped with the next GEMMs
     force_comm: bool = False         # run the DDP/FSDP collective path even at dp=1 (single-GPU RCCL check)
     comm_backend: str = "torch"      # torch (ProcessGroupNCCL/gloo) | native (csrc/comm.cpp RCCL layer)
+    tp_allreduce: str = "rccl"       # TP activation all-reduce: rccl (role communicator) | custom (csrc/car.hip)
     debug_sync: bool = False         # race screen: wait every collective at issue + device sync per layer
 
     @property
@@ -108,6 +109,8 @@ def add_extended_args(p: argparse.ArgumentParser) -> None:
     p.add_argument("--backend", choices=["auto", "nccl", "rccl", "gloo"], default="auto")
     p.add_argument("--comm", choices=["torch", "native"], default="torch",
                    help="communicator implementation for the role groups (native = C++ RCCL layer)")
+    p.add_argument("--tp_allreduce", choices=["rccl", "custom"], default="rccl",
+                   help="TP activation all-reduce: RCCL or the custom two-shot xGMI peer all-reduce")
     p.add_argument("--nprocs", type=int, default=0, help="ranks to spawn (0 = all visible GPUs)")
     p.add_argument("--dp", type=int, default=0)
     p.add_argument("--tp", type=int, default=0)

@@ -64,3 +64,67 @@ def test_processes_ipc(n, dtype, free_port):
     assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
     res = dict(q.get(timeout=10) for _ in range(n))
     assert all(res.values()), res
+
+
+def _tp_proc(rank, n, port, q):
+    import torch.distributed as dist
+
+    from dllm.models.ffn import init_ffn_layer
+    from dllm.parallel.engine import FFNTrainer
+    from dllm.parallel.mesh import Mesh
+    from dllm.utils.config import ModelConfig, TrainConfig
+    from dllm.utils.data import reference_mock_data
+
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=n)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    D, F, L, T = 256, 1024, 2, 512
+    gen = torch.Generator().manual_seed(7)
+    layers = [init_ffn_layer(D, F, gen) for _ in range(L)]
+    batches = list(reference_mock_data(torch.randint(100_000, (3,), generator=gen), T, D))
+    cfg = TrainConfig(model=ModelConfig(D, F, L), batch_size=1, seq_len=T, dtype="fp32", grad_dtype="fp32",
+                      lr=1e-2, dp=1, tp=n, tp_allreduce="custom", skip_input_grad=False)
+    mesh = Mesh.build(1, n, device=dev)
+    eng = FFNTrainer(cfg, mesh, dev)
+    assert eng.tp_car is not None
+    eng.load_full_params(layers)
+    for x, dy in batches:
+        eng.train_step(x.to(dev), dy.to(dev))
+    eng.tp_car.check()
+    loc = [{k: v.cpu() for k, v in p.items()} for p in eng.local_params()]
+    q.put((rank, loc))
+    dist.barrier()
+    mesh.destroy()
+    dist.destroy_process_group()
+
+
+def test_tp_engine_with_custom_allreduce(free_port):
+    """TP=2 training (two processes on the GPU, gloo only as the store) with the custom all-reduce for
+    the activation exchange equals single-device training up to reduction order (train_ffns.py:290-312)."""
+    from dllm.models import reference as R
+    from dllm.models.ffn import init_ffn_layer
+    from dllm.utils.data import reference_mock_data
+
+    n = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_tp_proc, args=(r, n, free_port, q)) for r in range(n)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(n))
+    for p in ps:
+        p.join(60)
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+    D, F, L, T = 256, 1024, 2, 512
+    gen = torch.Generator().manual_seed(7)
+    layers = [init_ffn_layer(D, F, gen) for _ in range(L)]
+    batches = list(reference_mock_data(torch.randint(100_000, (3,), generator=gen), T, D))
+    want = R.train_single(layers, batches, 1e-2)
+    for l in range(L):
+        w1 = torch.cat([res[r][l]["w1"] for r in range(n)], 0)
+        w2 = torch.cat([res[r][l]["w2"] for r in range(n)], 1)
+        for got, k in ((w1, "w1"), (w2, "w2")):
+            d_got = got.double() - layers[l][k].double()
+            d_want = want[l][k].double() - layers[l][k].double()
+            assert (d_got - d_want).norm() / d_want.norm() < 2e-3, (l, k)
