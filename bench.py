@@ -77,6 +77,8 @@ def parse():
     p.add_argument("--side_opt", type=int, default=0,
                    help="N=1: store wgrads and run SGD on a side stream over this many workgroups (0 = fuse the "
                         "update into the wgrad GEMM epilogue)")
+    p.add_argument("--phases", action="store_true",
+                   help="also report per-phase GPU time (forward / backward / optimizer tail) from HIP events")
     p.add_argument("--tp_allreduce", choices=["rccl", "custom"], default="rccl",
                    help="TP activation all-reduce: RCCL, or the custom two-shot xGMI peer all-reduce (csrc/car.hip)")
     p.add_argument("--gemm_variant", default="auto",
@@ -157,6 +159,8 @@ def main() -> int:
 
     for i in range(a.warmup):
         one_step(seed_base + i)
+    if a.phases and not cpu and graphed is None:
+        eng.enable_phase_timing(True)
     sync()
     comm.barrier(device=dev)
     t0 = time.perf_counter()
@@ -165,6 +169,7 @@ def main() -> int:
     sync()
     comm.barrier(device=dev)
     el = time.perf_counter() - t0
+    phases = {k: round(v / a.steps, 3) for k, v in eng.phase_summary().items()} if a.phases else None
     if world > 1:
         import torch.distributed as dist
 
@@ -195,6 +200,8 @@ def main() -> int:
         "plain_nt_gemm": "hipblaslt" if a.lib_plain_nt else "native", "gemm_variant": a.gemm_variant,
         "tp_allreduce": a.tp_allreduce,
     }
+    if phases:
+        rec["phase_ms_per_step"] = phases
     if a.force_comm:
         rec["note"] = "force_comm: DDP/FSDP collectives over size-1 RCCL communicators"
     if cpu:

@@ -510,6 +510,7 @@ class FFNTrainer:
         self.xs[0] = x
 
         # ---------------- forward ----------------
+        mark = self._mark("forward")
         if self.fsdp:
             self._fsdp_gather(0)
         for l in range(L):
@@ -552,7 +553,9 @@ class FFNTrainer:
                     comm.all_reduce(self.xs[l + 1], tpg, async_op=True).wait()
         y = self.xs[L]
 
+        self._unmark(mark)
         # ---------------- backward ----------------
+        mark = self._mark("backward")
         self._next_bucket = 0
         if self.fsdp and L >= 2 and self.ag_layer[(L - 2) % 2] != L - 2:
             # the forward left layers L-1 and L-2 in the ring; weights do not change until the
@@ -612,7 +615,9 @@ class FFNTrainer:
                     if at is not None and at > l:
                         self._zero_finish(b)
 
+        self._unmark(mark)
         # ---------------- optimizer ----------------
+        mark = self._mark("optimizer_tail")
         if self.zero:
             for b, at in enumerate(self.rs_issued_at):
                 if at is not None:
@@ -626,7 +631,42 @@ class FFNTrainer:
                 self._fsdp_finish_rs(slot)
         elif not self.fused_opt and not self.side_opt:
             self._opt(0, self.total)
+        self._unmark(mark)
         return y
+
+    # ------------------------------------------------------------------------------------------------
+    # phase annotation: roctx ranges (DLLM_ROCTX=1, rocprofv3 --marker-trace) and optional HIP-event
+    # phase timers (``enable_phase_timing``); both are no-ops otherwise
+    # ------------------------------------------------------------------------------------------------
+    def enable_phase_timing(self, on: bool = True) -> None:
+        from ..utils.profiling import PhaseTimer
+
+        self.phase_timer = PhaseTimer(on) if on else None
+
+    def phase_summary(self) -> dict:
+        pt = getattr(self, "phase_timer", None)
+        return pt.summary() if pt is not None else {}
+
+    def _mark(self, name: str):
+        from ..utils.profiling import roctx_push
+
+        roctx_push(name)
+        pt = getattr(self, "phase_timer", None)
+        if pt is None or not pt.enabled:
+            return (name, None)
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return (name, ev)
+
+    def _unmark(self, tok) -> None:
+        from ..utils.profiling import roctx_pop
+
+        roctx_pop()
+        name, ev = tok
+        if ev is not None:
+            end = torch.cuda.Event(enable_timing=True)
+            end.record()
+            self.phase_timer.events.append((name, ev, end))
 
 
 class _SPHooks(_Hooks):

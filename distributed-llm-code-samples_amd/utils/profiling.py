@@ -51,18 +51,38 @@ _ROCTX = None
 
 
 def _roctx():
+    """The roctx library rocprofv3 intercepts (ROCm's rocprofiler-sdk roctx), else torch's legacy one."""
     global _ROCTX
     if _ROCTX is None:
-        try:
-            import ctypes
+        import ctypes
 
-            d = os.path.join(os.path.dirname(torch.__file__), "lib", "libroctx64.so")
-            _ROCTX = ctypes.CDLL(d) if os.path.exists(d) else False
-            if _ROCTX:
-                _ROCTX.roctxRangePushA.argtypes = [ctypes.c_char_p]
-        except OSError:
-            _ROCTX = False
+        _ROCTX = False
+        rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+        for d in (os.path.join(rocm, "lib", "librocprofiler-sdk-roctx.so.1"),
+                  os.path.join(os.path.dirname(torch.__file__), "lib", "libroctx64.so")):
+            if os.path.exists(d):
+                try:
+                    _ROCTX = ctypes.CDLL(d)
+                    _ROCTX.roctxRangePushA.argtypes = [ctypes.c_char_p]
+                    break
+                except (OSError, AttributeError):
+                    _ROCTX = False
     return _ROCTX
+
+
+def roctx_push(name: str) -> None:
+    """Open a roctx range when DLLM_ROCTX=1 (no-op otherwise)."""
+    if os.environ.get("DLLM_ROCTX") == "1":
+        lib = _roctx()
+        if lib:
+            lib.roctxRangePushA(name.encode())
+
+
+def roctx_pop() -> None:
+    if os.environ.get("DLLM_ROCTX") == "1":
+        lib = _roctx()
+        if lib:
+            lib.roctxRangePop()
 
 
 @contextlib.contextmanager
