@@ -214,6 +214,14 @@ class FFNTrainer:
                     self.buckets.append((start, end, i))
                     start = end
             self.bucket_work = [None] * len(self.buckets)
+            self.weight_buckets = {(l, n): sorted(b for b, (s_, e_, _) in enumerate(self.buckets)
+                                                  if s_ < self.entry[(l, n)].offset + self.entry[(l, n)].numel
+                                                  and self.entry[(l, n)].offset < e_)
+                                   for l in range(L) for n in ("w1", "w2")}
+            # the step-boundary buckets' optimizer (+ ZeRO all-gather) run on a side stream so the next
+            # step's first GEMM does not queue behind the last collective; the forward waits per weight
+            self.opt_stream = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
+            self.ddp_done = [None] * len(self.buckets)
         if self.zero:
             # rank r owns [s + r*(e-s)/d, s + (r+1)*(e-s)/d) of every bucket
             self.gshard = torch.zeros(self.total // d, dtype=self.gd, device=dev)
@@ -225,14 +233,6 @@ class FFNTrainer:
                 goff += n
             self.ag_pending = [None] * len(self.buckets)
             self.rs_issued_at = [None] * len(self.buckets)
-            self.weight_buckets = {(l, n): sorted(b for b, (s_, e_, _) in enumerate(self.buckets)
-                                                  if s_ < self.entry[(l, n)].offset + self.entry[(l, n)].numel
-                                                  and self.entry[(l, n)].offset < e_)
-                                   for l in range(L) for n in ("w1", "w2")}
-            # the final buckets' optimizer + all-gather run on a side stream so the next step's first
-            # GEMM does not queue behind the last reduce-scatter (ordering: the forward waits for the
-            # all-gather, which was issued after the update on that stream)
-            self.opt_stream = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
             self._master_synced = True
         self._entry_index = {(e.layer, e.name): i for i, e in enumerate(self.entries)}
         self._next_bucket = 0
@@ -278,6 +278,7 @@ class FFNTrainer:
         if self.zero:
             self.zero_sync_state()
         self.side_sync()
+        self.ddp_sync()
         out = {"params": self.master}
         if self.cfg.optimizer == "adam":
             out["adam_m"], out["adam_v"] = self.adam_m, self.adam_v
@@ -322,6 +323,7 @@ class FFNTrainer:
         """This TP rank's full local (unsharded over dp) fp32 tensors of a flat buffer, w1 de-interleaved.
         Collective over the dp group under FSDP."""
         self.side_sync()
+        self.ddp_sync()
         src = self.master if flat is None else flat
         out = []
         for l in range(self.L):
@@ -445,6 +447,18 @@ class FFNTrainer:
         self.ag_pending[b] = comm.all_gather_into(self.copy[s_:e_], src, self.mesh.group("dp_ag"), async_op=True)
         self.rs_issued_at[b] = None
 
+    def _ddp_wait(self, l: int, name: str) -> None:
+        for b in self.weight_buckets[(l, name)]:
+            ev = self.ddp_done[b]
+            if ev is not None:
+                torch.cuda.current_stream(self.device).wait_event(ev)
+                self.ddp_done[b] = None
+
+    def ddp_sync(self) -> None:
+        if self.ddp:
+            for (l, n) in list(self.weight_buckets):
+                self._ddp_wait(l, n)
+
     def _side_wait(self, l: int, name: str) -> None:
         ev = self.opt_done.pop((l, name), None)
         if ev is not None:
@@ -524,6 +538,8 @@ class FFNTrainer:
                         self._zero_wait_ag(b)
                 if self.side_opt:
                     self._side_wait(l, "w1")
+                if self.ddp:
+                    self._ddp_wait(l, "w1")
                 w1, w2 = self.copy_view(l, "w1"), self.copy_view(l, "w2")
             a = self.acts_a[l if keep else 0]
             h = (self.acts_h[l if keep else 0]) if self.need_h else None
@@ -533,6 +549,8 @@ class FFNTrainer:
                         self._zero_wait_ag(b)
                 if self.side_opt:
                     self._side_wait(l, "w2")
+                if self.ddp:
+                    self._ddp_wait(l, "w2")
                 xin = self.xs_full[l] if keep else self.xfull
                 comm.all_gather_into(xin, self.xs[l], tpg, async_op=True).wait()
                 layer_fwd(xin, w1, w2, act, gated, a, h, self.yfull)
@@ -546,6 +564,9 @@ class FFNTrainer:
                 elif self.side_opt:
                     def before2(l=l):
                         self._side_wait(l, "w2")
+                elif self.ddp:
+                    def before2(l=l):
+                        self._ddp_wait(l, "w2")
                 layer_fwd(self.xs[l], w1, w2, act, gated, a, h, self.xs[l + 1], before_fwd2=before2)
                 if self.tp_car is not None:
                     self.tp_car.all_reduce(self.xs[l + 1])
@@ -623,9 +644,21 @@ class FFNTrainer:
                 if at is not None:
                     self._zero_finish(b, side=True)
         elif self.ddp:
+            # buckets completed before layer 0's: update on the compute stream; layer 0's (the step
+            # boundary, whose all-reduce was issued last) on the side stream, waited per weight
+            tail = set(self.weight_buckets[(0, "w1")]) | set(self.weight_buckets[(0, "w2")])
             for b, (s, e, _) in enumerate(self.buckets):
-                self.bucket_work[b].wait()
-                self._opt(s, e)
+                if b in tail and self.opt_stream is not None:
+                    self.opt_stream.wait_stream(torch.cuda.current_stream(self.device))
+                    with torch.cuda.stream(self.opt_stream):
+                        self.bucket_work[b].wait()
+                        self._opt(s, e)
+                        ev = torch.cuda.Event()
+                        ev.record(self.opt_stream)
+                    self.ddp_done[b] = ev
+                else:
+                    self.bucket_work[b].wait()
+                    self._opt(s, e)
         elif self.fsdp:
             for slot in ((L - 1) % 2, L % 2):
                 self._fsdp_finish_rs(slot)
