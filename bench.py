@@ -86,6 +86,8 @@ def parse():
                    help="bf16 GEMM main-loop schedule (auto = 4-phase staggered when K % 128 == 0)")
     p.add_argument("--lib_plain_nt", action="store_true",
                    help="run the plain forward GEMM y = a·W2ᵀ (no epilogue) on hipBLASLt; all fused GEMMs stay native")
+    p.add_argument("--tpb", type=int, default=0,
+                   help="tiles per block of the 8-phase GEMM (persistent blocks; 0 = library default)")
     p.add_argument("--force_comm", action="store_true",
                    help="exercise the RCCL DDP/FSDP path at N=1 (size-1 communicators, unfused optimizer)")
     return p.parse_args()
@@ -123,6 +125,10 @@ def main() -> int:
         from dllm.ops.gemm import set_bf16_variant
 
         set_bf16_variant(a.gemm_variant)
+    if a.tpb and not cpu:
+        from dllm.ops.gemm import set_tiles_per_block
+
+        set_tiles_per_block(a.tpb)
     if a.lib_plain_nt:
         from dllm.ops.gemm import set_library_plain_nt
 
@@ -198,6 +204,7 @@ def main() -> int:
         "tflops_per_gpu": round(tflops, 1), "mfu_dense": round(tflops / PEAK_TFLOPS[a.dtype], 4),
         "peak_hbm_gib": round(peak_gib, 2), "finite": finite, "comm": a.comm, "hip_graph": bool(a.graph),
         "plain_nt_gemm": "hipblaslt" if a.lib_plain_nt else "native", "gemm_variant": a.gemm_variant,
+        "gemm_tiles_per_block": a.tpb or "default",
         "tp_allreduce": a.tp_allreduce,
     }
     if phases:

@@ -46,6 +46,8 @@ struct GemmArgs {
   float* opt_v;
   // split-K: ksplit > 1 -> the main kernel writes fp32 partials C + split*M*ldc (C = workspace)
   int ksplit;
+  // tiles per block of a persistent 8-phase kernel (PERS instantiations only)
+  int tpb;
 };
 
 // ----------------------------------------------------------------------------------------------
@@ -229,13 +231,15 @@ __device__ __forceinline__ void unpair_bf16(uint4 v, f32x4_t& a, f32x4_t& b) {
 // row group rg = QM*8 + QN*4 + mt (16 per wave), 2 column groups (nt) each.
 template <int EPI, typename OutT, int ACT>
 __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2][2][4][2], int m0, int n0,
-                                             int wr, int wc, int lane) {
+                                             int wr, int wc, int lane, void* Cp) {
   constexpr bool BF = std::is_same<OutT, uint16_t>::value;
   using R = Raw4<OutT>;
   using RT = typename std::conditional<BF, uint4, f32x4_t>::type;  // bf16: one paired 16-B load per row group
   using RF = Raw4<float>;
   constexpr int WR = BF ? 4 : 8;  // VGPRs per row group and loaded operand
-  constexpr int COST = EPI == EPI_DACT ? WR : EPI == EPI_DGLU ? 8 * (BF ? 2 : 4) : EPI == EPI_STORE ? WR
+  // (the beta != 0 store path is off the FFN hot path: small batches keep the persistent kernel's
+  // in-loop epilogue within the register budget)
+  constexpr int COST = EPI == EPI_DACT ? WR : EPI == EPI_DGLU ? 8 * (BF ? 2 : 4) : EPI == EPI_STORE ? 4 * WR
                      : EPI == EPI_SGD ? 8 : EPI == EPI_ADAM ? 24 : 0;
   constexpr int RB = epi_batch(COST);
   const int pc = pair_col(lane);
@@ -269,18 +273,18 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
     if (p.beta == 0.f) {
 #pragma unroll
       for (int rg = 0; rg < 16; ++rg)
-        store_rg(p.C, p.ldc, DLLM_M(rg), DLLM_NB(rg), DLLM_ACC(rg, 0) * p.alpha, DLLM_ACC(rg, 1) * p.alpha);
+        store_rg(Cp, p.ldc, DLLM_M(rg), DLLM_NB(rg), DLLM_ACC(rg, 0) * p.alpha, DLLM_ACC(rg, 1) * p.alpha);
     } else {
 #pragma unroll
       for (int b0 = 0; b0 < 16; b0 += RB) {
         RT L[RB][2];
 #pragma unroll
-        for (int r = 0; r < RB; ++r) load_rg(p.C, p.ldc, DLLM_M(b0 + r), DLLM_NB(b0 + r), L[r]);
+        for (int r = 0; r < RB; ++r) load_rg(Cp, p.ldc, DLLM_M(b0 + r), DLLM_NB(b0 + r), L[r]);
 #pragma unroll
         for (int r = 0; r < RB; ++r) {
           f32x4_t c0, c1;
           decode_rg(L[r], c0, c1);
-          store_rg(p.C, p.ldc, DLLM_M(b0 + r), DLLM_NB(b0 + r), DLLM_ACC(b0 + r, 0) * p.alpha + p.beta * c0,
+          store_rg(Cp, p.ldc, DLLM_M(b0 + r), DLLM_NB(b0 + r), DLLM_ACC(b0 + r, 0) * p.alpha + p.beta * c0,
                    DLLM_ACC(b0 + r, 1) * p.alpha + p.beta * c1);
         }
       }
@@ -299,7 +303,7 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
         a[e] = actf<ACT>(p.act, a[e]);
         b[e] = actf<ACT>(p.act, b[e]);
       }
-      store_rg(p.C, p.ldc, DLLM_M(rg), DLLM_NB(rg), a, b);
+      store_rg(Cp, p.ldc, DLLM_M(rg), DLLM_NB(rg), a, b);
     }
   } else if constexpr (EPI == EPI_DACT) {
 #pragma unroll
@@ -317,7 +321,7 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
           a[e] *= actg<ACT>(p.act, h0[e]);
           b[e] *= actg<ACT>(p.act, h1[e]);
         }
-        store_rg(p.C, p.ldc, DLLM_M(b0 + r), DLLM_NB(b0 + r), a, b);
+        store_rg(Cp, p.ldc, DLLM_M(b0 + r), DLLM_NB(b0 + r), a, b);
       }
     }
   } else if constexpr (EPI == EPI_GLU) {
@@ -334,7 +338,7 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
       f32x4_t a;
 #pragma unroll
       for (int e = 0; e < 4; ++e) a[e] = actf<ACT>(p.act, g[e]) * u[e];
-      Vec4<OutT>::store(p.C, (long)DLLM_M(rg) * p.ldc + (nb >> 5) * 16 + (nb & 15), a);
+      Vec4<OutT>::store(Cp, (long)DLLM_M(rg) * p.ldc + (nb >> 5) * 16 + (nb & 15), a);
     }
   } else if constexpr (EPI == EPI_DGLU) {
     // acc = da over the de-interleaved F axis; aux / C interleaved [g|u] 16-column blocks
@@ -364,8 +368,8 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
             dg[e] = da[e] * u[e] * actg<ACT>(p.act, g[e]);
           }
           const long base = (long)DLLM_M(b0 + r) * p.ldc + ng;
-          Vec4<OutT>::store(p.C, base, dg);
-          Vec4<OutT>::store(p.C, base + 16, du);
+          Vec4<OutT>::store(Cp, base, dg);
+          Vec4<OutT>::store(Cp, base + 16, du);
         }
     }
   } else if constexpr (EPI == EPI_SGD) {
@@ -375,7 +379,7 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
 #pragma unroll
       for (int r = 0; r < RB; ++r)
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) W[r][nt] = RF::load(p.C, (long)DLLM_M(b0 + r) * p.ldc + DLLM_N(b0 + r, nt));
+        for (int nt = 0; nt < 2; ++nt) W[r][nt] = RF::load(Cp, (long)DLLM_M(b0 + r) * p.ldc + DLLM_N(b0 + r, nt));
 #pragma unroll
       for (int r = 0; r < RB; ++r)
 #pragma unroll
@@ -384,7 +388,7 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
 #pragma unroll
           for (int e = 0; e < 4; ++e)
             W[r][nt][e] = __fadd_rn(W[r][nt][e], __fmul_rn(-p.lr, __fmul_rn(p.alpha, g[e])));
-          Vec4<float>::store(p.C, (long)DLLM_M(b0 + r) * p.ldc + DLLM_N(b0 + r, nt), W[r][nt]);
+          Vec4<float>::store(Cp, (long)DLLM_M(b0 + r) * p.ldc + DLLM_N(b0 + r, nt), W[r][nt]);
         }
       if (p.aux_out) {
 #pragma unroll
@@ -401,7 +405,7 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) {
           const long ci = (long)DLLM_M(b0 + r) * p.ldc + DLLM_N(b0 + r, nt);
-          W[r][nt] = RF::load(p.C, ci);
+          W[r][nt] = RF::load(Cp, ci);
           Mm[r][nt] = RF::load(p.opt_m, ci);
           Vv[r][nt] = RF::load(p.opt_v, ci);
         }
@@ -419,7 +423,7 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
             W[r][nt][e] = W[r][nt][e] - p.lr * (mh / (sqrtf(vh) + p.eps) + p.wd * W[r][nt][e]);
           }
           const long ci = (long)DLLM_M(b0 + r) * p.ldc + DLLM_N(b0 + r, nt);
-          Vec4<float>::store(p.C, ci, W[r][nt]);
+          Vec4<float>::store(Cp, ci, W[r][nt]);
           Vec4<float>::store(p.opt_m, ci, Mm[r][nt]);
           Vec4<float>::store(p.opt_v, ci, Vv[r][nt]);
         }
@@ -671,6 +675,20 @@ __device__ __forceinline__ bf16x8_t cat_tr(s16x4_t lo, s16x4_t hi) {
   s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(bf16x8_t, v);
 }
+// A fresh copy of the kernel arguments, loaded (s_load from the kernarg segment) at the call site.  hipcc
+// does not rematerialise kernarg loads, so arguments used only by a persistent kernel's per-tile epilogue
+// would otherwise stay live in SGPRs across the main loop (and spill).  The empty asm makes the pointer
+// opaque so the loads cannot be hoisted.
+__device__ __forceinline__ GemmArgs reload_args() {
+  typedef const __attribute__((address_space(4))) uint32_t* KargWords;
+  KargWords pa = (KargWords)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(pa));
+  struct Words { uint32_t w[sizeof(GemmArgs) / 4]; } r;
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(GemmArgs) / 4); ++i) r.w[i] = pa[i];
+  return __builtin_bit_cast(GemmArgs, r);
+}
+
 #define DLLM_LDS_WAIT()                                   \
   do {                                                    \
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");    \
@@ -684,7 +702,7 @@ __device__ __forceinline__ bf16x8_t cat_tr(s16x4_t lo, s16x4_t hi) {
 // NPH = 8: the 8-phase schedule below (one quadrant = 16 MFMAs per wave per barrier interval).
 // NPH = 4: half-tile phases (two quadrants = 32 MFMAs per interval, two half-tiles restaged per phase):
 // halves the barrier count per MFMA (see the NPH == 4 loop).
-template <int LAYOUT, int EPI, typename OutT, bool STAGGER, int ABL = 0, int ACT = -1, int NPH = 8>
+template <int LAYOUT, int EPI, typename OutT, bool STAGGER, int ABL = 0, int ACT = -1, int NPH = 8, bool PERS = false>
 __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
   // slot(op, hh, buf) = ((op*2 + hh)*2 + buf) * 16 KiB: A in [0, 64K), B in [64K, 128K), so every
   // fragment read is base + a 16-bit immediate
@@ -694,22 +712,32 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wid >> 2, wc = wid & 3;
   const int tiles_m = p.M / BT_M, tiles_n = p.N / BT_N;
-  const int bid0 = xcd_remap(blockIdx.x, gridDim.x);
   const int ntiles = tiles_m * tiles_n;
-  const int split = bid0 / ntiles, bid = bid0 % ntiles;  // split-K slice (0 when ksplit == 1)
-  const int width = p.group_m * tiles_n;
-  const int first_m = (bid / width) * p.group_m;
-  const int gsz = min(tiles_m - first_m, p.group_m);
-  const int tm = first_m + (bid % width) % gsz;
-  const int tn = (bid % width) / gsz;
-  const int m0 = tm * BT_M, n0 = tn * BT_N;
-
+  const int total = ntiles * p.ksplit;  // tile slots (split-K slices count as tiles)
+  // Persistent blocks (PERS, NPH == 8, p.tpb > 1): block b runs slots b, b + G, b + 2G, ... (G = gridDim.x,
+  // a multiple of the 8 XCDs, so every slot of a block maps to the block's own XCD under the remap).  Slot ->
+  // tile goes through the XCD remap over ALL slots: the same tile placement and order as one block per tile.
+  // A separate instantiation, so the one-tile-per-block kernels carry none of its state.
+  const bool pers = PERS && NPH == 8 && p.tpb > 1;
+  int slot = blockIdx.x;
+  // Per-slot helpers take the argument block explicitly: inside the slot loop they are called with a fresh
+  // reload_args() copy, so the epilogue's arguments are loaded where they are used instead of being kept
+  // live in SGPRs across the whole main loop.
+  auto tile_of = [&](const GemmArgs& q, int s, int& sp, int& tm0, int& tn0) {
+    const int tm_ = q.M / BT_M, tn_ = q.N / BT_N, nt = tm_ * tn_;
+    const int bid0 = xcd_remap(s, pers ? nt * q.ksplit : (int)gridDim.x);
+    sp = bid0 / nt;  // split-K slice (0 when ksplit == 1)
+    const int bid = bid0 % nt;
+    const int width = q.group_m * tn_;
+    const int first_m = (bid / width) * q.group_m;
+    const int gsz = min(tm_ - first_m, q.group_m);
+    tm0 = (first_m + (bid % width) % gsz) * BT_M;
+    tn0 = ((bid % width) / gsz) * BT_N;
+  };
   constexpr bool A_KC = (ABL & 1) ? true : (LAYOUT != L_TN);
   constexpr bool B_KC = (ABL & 2) ? true : (LAYOUT == L_NT);
   constexpr bool A_RKC = (ABL & 4) ? true : (LAYOUT != L_TN);
   constexpr bool B_RKC = (ABL & 8) ? true : (LAYOUT == L_NT);
-  const uint16_t* Ag = (const uint16_t*)p.A + (A_KC ? (long)m0 * p.lda : (long)m0);
-  const uint16_t* Bg = (const uint16_t*)p.B + (B_KC ? (long)n0 * p.ldb : (long)n0);
   long aoff[2], boff[2];
   if constexpr (A_KC) kc_half_offsets(p.lda, wid, lane, aoff); else mc_half_offsets(p.lda, wid, lane, aoff);
   if constexpr (B_KC) kc_half_offsets(p.ldb, wid, lane, boff); else mc_half_offsets(p.ldb, wid, lane, boff);
@@ -718,15 +746,51 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
   const long a_hstep = A_KC ? 128L * p.lda : 128L;
   const long b_hstep = B_KC ? 128L * p.ldb : 128L;
   const int nk = p.K / BT_K / p.ksplit;  // even (host guarantees (K/64) % (2*ksplit) == 0)
-  const int kt0 = split * nk;
+  // K-tile 0 of a slot's A / B panels
+  auto a_base = [&](const GemmArgs& q, int s) {
+    int sp, tm0, tn0;
+    tile_of(q, s, sp, tm0, tn0);
+    return (const uint16_t*)q.A + (A_KC ? (long)tm0 * q.lda : (long)tm0) + (long)sp * nk * a_kstep;
+  };
+  auto b_base = [&](const GemmArgs& q, int s) {
+    int sp, tm0, tn0;
+    tile_of(q, s, sp, tm0, tn0);
+    return (const uint16_t*)q.B + (B_KC ? (long)tn0 * q.ldb : (long)tn0) + (long)sp * nk * b_kstep;
+  };
+  // epilogue of a slot; split-K slices write fp32 partial planes C + split*M*ldc
+  auto slot_epilogue = [&](int s, f32x4_t (&ac)[2][2][4][2]) {
+    const GemmArgs q = reload_args();
+    int sp, tm0, tn0;
+    tile_of(q, s, sp, tm0, tn0);
+    void* out = q.C;
+    if constexpr (EPI == EPI_STORE)
+      if (q.ksplit > 1) out = (char*)q.C + (long)sp * q.M * q.ldc * sizeof(OutT);
+    epilogue_256<EPI, OutT, ACT>(q, ac, tm0, tn0, wr, wc, lane, out);
+  };
+  // next slot of this block (>= total: none)
+  int next_slot = total;
+  auto begin_tile = [&]() { next_slot = pers ? slot + (int)gridDim.x : total; };
+  begin_tile();
 
-  auto stage = [&](int op, int hh, int kt, int buf) {
-    kt = kt0 + min(kt, nk - 1);
+  // stage half hh of the K-tile at `src` (K-tile base of operand op) into buffer buf
+  auto stage_at = [&](int op, int hh, const uint16_t* src, int buf) {
     DLLM_LDS char* dst = lds + ((op * 2 + hh) * 2 + buf) * HT;
-    const uint16_t* src = op == 0 ? Ag + kt * a_kstep + hh * a_hstep : Bg + kt * b_kstep + hh * b_hstep;
+    src += op == 0 ? hh * a_hstep : hh * b_hstep;
     const long* off = op == 0 ? aoff : boff;
     glds16(src + off[0], dst + wid * 1024);
     glds16(src + off[1], dst + (wid + 8) * 1024);
+  };
+  // 8-phase loop: running prefetch pointers at K-tile 2*it + 2 of the current slot; in the final iteration
+  // they move to the NEXT slot's K-tile 0, so the last iteration's prefetches (K-tiles "nk", "nk+1") are
+  // exactly the next slot's prologue -- the pipeline runs on across tiles without a drain and the epilogue
+  // overlaps those loads.  Without a next slot they re-load this slot's K-tiles nk-2, nk-1 into buffers
+  // that are never read again, so every phase issues the same loads.
+  const uint16_t* Apf = a_base(p, slot);
+  const uint16_t* Bpf = b_base(p, slot);
+  // one-tile kernels (NPH == 4, 2-stage-compatible paths): K-tile kt of the block's only slot, clamped
+  auto stage = [&](int op, int hh, int kt, int buf) {
+    kt = min(kt, nk - 1);
+    stage_at(op, hh, op == 0 ? Apf + kt * a_kstep : Bpf + kt * b_kstep, buf);
   };
 
   // ---- per-lane fragment base addresses (LDS byte addresses) ----
@@ -899,77 +963,105 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
   // prologue: tile 0 -> even buffer (4 half-tiles), tile 1 -> odd (A0, B0, B1; A1 comes at P0)
   stage(0, 0, 0, 0); stage(1, 0, 0, 0); stage(1, 1, 0, 0); stage(0, 1, 0, 0);
   stage(0, 0, 1, 1); stage(1, 0, 1, 1); stage(1, 1, 1, 1);
+  Apf += 2 * a_kstep;
+  Bpf += 2 * b_kstep;
   asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   DLLM_BARRIER();
   if constexpr (STAGGER) {
     if (wr == 1) DLLM_BARRIER();
   }
 
+  for (;;) {  // slots of this block (one pass unless persistent)
   for (int it = 0; it < nk / 2; ++it) {
-    const int te = 2 * it, to = 2 * it + 1;
-#define DLLM_PHASE_END(VMWAIT)                                       \
+#define DLLM_PHASE_END(VMWAIT)                                      \
   if (VMWAIT) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");       \
   DLLM_LDS_WAIT();                                                   \
   DLLM_BARRIER();
-    // ---- even buffer (tile te) ----
+    // ---- even buffer (K-tile 2it) ----
     read_a(I0{}, I0{}); read_b(I0{}, I0{}, fb0);
-    stage(0, 1, to, 1);                        // P0: A1 odd
+    stage_at(0, 1, Apf - a_kstep, 1);          // P0: A1 odd (K-tile 2it+1)
+    if (it == nk / 2 - 1) {
+      // last iteration: the remaining prefetches are the next slot's K-tiles 0/1 (or harmless re-loads)
+      if (next_slot < total) {
+        const GemmArgs q = reload_args();
+        Apf = a_base(q, next_slot);
+        Bpf = b_base(q, next_slot);
+      } else {
+        Apf -= 2 * a_kstep;
+        Bpf -= 2 * b_kstep;
+      }
+    }
     DLLM_PHASE_END(false)
     fin_a(); fin_b(fb0);
     mfma_quad(acc[0][0], fb0);
     DLLM_BARRIER();
     read_b(I1{}, I0{}, fb1);
-    stage(0, 0, te + 2, 0);                    // P1: A0 even
+    stage_at(0, 0, Apf, 0);                    // P1: A0 even (K-tile 2it+2)
     DLLM_PHASE_END(false)
     fin_b(fb1);
     mfma_quad(acc[0][1], fb1);
     DLLM_BARRIER();
     read_a(I1{}, I0{});
-    stage(1, 0, te + 2, 0);                    // P2: B0 even
+    stage_at(1, 0, Bpf, 0);                    // P2: B0 even
     DLLM_PHASE_END(false)
     fin_a();
     mfma_quad(acc[1][1], fb1);
     DLLM_BARRIER();
-    stage(1, 1, te + 2, 0);                    // P3: B1 even
+    stage_at(1, 1, Bpf, 0);                    // P3: B1 even
     DLLM_PHASE_END(true)
     mfma_quad(acc[1][0], fb0);
     DLLM_BARRIER();
-    // ---- odd buffer (tile to) ----
+    // ---- odd buffer (K-tile 2it+1) ----
     read_a(I0{}, I1{}); read_b(I0{}, I1{}, fb0);
-    stage(0, 1, te + 2, 0);                    // P4: A1 even
+    stage_at(0, 1, Apf, 0);                    // P4: A1 even
     DLLM_PHASE_END(false)
     fin_a(); fin_b(fb0);
     mfma_quad(acc[0][0], fb0);
     DLLM_BARRIER();
     read_b(I1{}, I1{}, fb1);
-    stage(0, 0, to + 2, 1);                    // P5: A0 odd
+    stage_at(0, 0, Apf + a_kstep, 1);          // P5: A0 odd (K-tile 2it+3)
     DLLM_PHASE_END(false)
     fin_b(fb1);
     mfma_quad(acc[0][1], fb1);
     DLLM_BARRIER();
     read_a(I1{}, I1{});
-    stage(1, 0, to + 2, 1);                    // P6: B0 odd
+    stage_at(1, 0, Bpf + b_kstep, 1);          // P6: B0 odd
     DLLM_PHASE_END(false)
     fin_a();
     mfma_quad(acc[1][1], fb1);
     DLLM_BARRIER();
-    stage(1, 1, to + 2, 1);                    // P7: B1 odd
+    stage_at(1, 1, Bpf + b_kstep, 1);          // P7: B1 odd
     DLLM_PHASE_END(true)
     mfma_quad(acc[1][0], fb0);
     DLLM_BARRIER();
+    Apf += 2 * a_kstep;
+    Bpf += 2 * b_kstep;
 #undef DLLM_PHASE_END
   }
+  if (next_slot >= total) break;
+  // Persistent: the next slot's K-tiles 0/1 are landed (even buffer) or in flight (odd half-tiles) and
+  // Apf/Bpf already point at its K-tile 2; this slot's epilogue runs meanwhile.  It touches no LDS and
+  // has no barrier, so the (staggered) barrier sequence continues unchanged into the next slot's P0; its
+  // memory operations are older than the next slot's P0-P3 stages and are retired by P3's counted wait.
+  slot_epilogue(slot, acc);
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int d = 0; d < 2; ++d) acc[a][b][c][d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  slot = next_slot;
+  begin_tile();
+  }  // slots
   }  // NPH == 8
   if constexpr (STAGGER) {
     if (wr == 0) DLLM_BARRIER();
   }
-  // drain the clamped tail prefetches before the block can release its LDS
+  // drain the tail prefetches before the block can release its LDS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if constexpr (EPI == EPI_STORE) {
-    if (p.ksplit > 1) p.C = (char*)p.C + (long)split * p.M * p.ldc * sizeof(OutT);
-  }
-
-  epilogue_256<EPI, OutT, ACT>(p, acc, m0, n0, wr, wc, lane);
+  slot_epilogue(slot, acc);
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -1208,6 +1300,39 @@ __global__ __launch_bounds__(256) void splitk_reduce(GemmArgs p, const float* ws
 // variant: 0 = auto (8-phase staggered when K % 128 == 0, else 2-stage), 1 = 2-stage, 2 = 8-phase, 3 = 8-phase staggered,
 // 4 = 4-phase (half-tile phases) staggered
 static int g_bf16_variant = 0;
+// Persistent 8-phase blocks (the FFN's hot GEMMs): a block runs up to g_tpb output tiles back to back, the next
+// tile's first K-tiles prefetched under the current tile's epilogue (no pipeline drain, no block relaunch per
+// tile).  g_tpb <= 1: one block per tile.  The grid never drops below one block per CU, so g_tpb is capped at
+// tiles / CUs; at the default of 2 a block delayed by a concurrent kernel (an overlapped RCCL collective)
+// holds back at most two tiles.
+static int g_tpb = 2;
+constexpr int MAX_DEV = 64;
+static int g_num_cu[MAX_DEV] = {};
+
+static int num_cu() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DEV) return 0;
+  if (g_num_cu[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n = -1;
+    g_num_cu[dev] = n;
+  }
+  return g_num_cu[dev];
+}
+
+// grid of a persistent 8-phase launch over nb tile slots; sets a.tpb (1: launch the one-tile kernel instead).
+// Persistent grids are a multiple of the 8 XCDs (every slot of a block maps to the block's own XCD).
+static int grid_8ph(GemmArgs& a, int nb) {
+  a.tpb = 1;
+  const int ncu = num_cu();
+  if (g_tpb <= 1 || ncu <= 0) return nb;
+  const int t = std::min(g_tpb, nb / ncu);
+  if (t <= 1) return nb;
+  const int g = ((nb + t - 1) / t + 7) / 8 * 8;
+  if (g >= nb) return nb;
+  a.tpb = t;
+  return g;
+}
 
 // main kernel writes partials into the workspace, then the reduction applies the epilogue
 template <int L, int E>
@@ -1218,6 +1343,7 @@ static hipError_t launch_splitk(const GemmArgs& a, int out_dt, float* ws, hipStr
   w.alpha = 1.f;
   w.beta = 0.f;
   const int nb = (a.M / BT_M) * (a.N / BT_N) * a.ksplit;
+  w.tpb = 1;
   if (g_bf16_variant == 4) hipLaunchKernelGGL((gemm_bf16_8ph<L, EPI_STORE, float, true, 0, -1, 4>), dim3(nb), dim3(512), 0, s, w);
   else hipLaunchKernelGGL((gemm_bf16_8ph<L, EPI_STORE, float, true>), dim3(nb), dim3(512), 0, s, w);
   hipError_t e = hipGetLastError();
@@ -1237,19 +1363,43 @@ static float* g_splitk_ws = nullptr;  // set per call by dllm_gemm (caller-owned
 
 // staggered 8-phase launch; the FFN's own activation epilogues (NT act/glu forward, NN dact/dglu
 // dgrad, bf16 out) get a compile-time activation, everything else the runtime switch
+// persistent instantiations exist for the FFN's own GEMMs only: bf16-out forward / dgrad GEMMs with a
+// compile-time activation (or none), and the weight-gradient GEMMs (stored gradients, fused optimizers)
+template <int L, int E, typename OutT>
+constexpr bool persistent_kernel() {
+  constexpr bool bf = std::is_same<OutT, uint16_t>::value;
+  if constexpr (L == L_NT) return bf && (E == EPI_ACT || E == EPI_GLU || E == EPI_STORE);
+  if constexpr (L == L_NN) return bf && (E == EPI_DACT || E == EPI_DGLU || E == EPI_STORE);
+  return E == EPI_STORE || E == EPI_SGD || E == EPI_ADAM;
+}
+
+template <int L, int E, typename OutT, int ACT, int NPH>
+static void launch_8ph_act(const GemmArgs& a0, int nb0, hipStream_t s) {
+  if constexpr (NPH == 8 && persistent_kernel<L, E, OutT>() && (ACT >= 0 || !(E == EPI_ACT || E == EPI_GLU ||
+                                                                                 E == EPI_DACT || E == EPI_DGLU))) {
+    GemmArgs a = a0;
+    const int nb = grid_8ph(a, nb0);
+    if (a.tpb > 1) {
+      hipLaunchKernelGGL((gemm_bf16_8ph<L, E, OutT, true, 0, ACT, NPH, true>), dim3(nb), dim3(512), 0, s, a);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((gemm_bf16_8ph<L, E, OutT, true, 0, ACT, NPH>), dim3(nb0), dim3(512), 0, s, a0);
+}
+
 template <int L, int E, typename OutT, int NPH>
 static void launch_8ph_stagger(const GemmArgs& a, int nb, hipStream_t s) {
   constexpr bool fwd = L == L_NT && (E == EPI_ACT || E == EPI_GLU);
   constexpr bool bwd = L == L_NN && (E == EPI_DACT || E == EPI_DGLU);
   if constexpr ((fwd || bwd) && std::is_same<OutT, uint16_t>::value) {
     switch (a.act) {
-      case ACT_RELU: hipLaunchKernelGGL((gemm_bf16_8ph<L, E, OutT, true, 0, ACT_RELU, NPH>), dim3(nb), dim3(512), 0, s, a); return;
-      case ACT_SILU: hipLaunchKernelGGL((gemm_bf16_8ph<L, E, OutT, true, 0, ACT_SILU, NPH>), dim3(nb), dim3(512), 0, s, a); return;
-      case ACT_GELU: hipLaunchKernelGGL((gemm_bf16_8ph<L, E, OutT, true, 0, ACT_GELU, NPH>), dim3(nb), dim3(512), 0, s, a); return;
+      case ACT_RELU: launch_8ph_act<L, E, OutT, ACT_RELU, NPH>(a, nb, s); return;
+      case ACT_SILU: launch_8ph_act<L, E, OutT, ACT_SILU, NPH>(a, nb, s); return;
+      case ACT_GELU: launch_8ph_act<L, E, OutT, ACT_GELU, NPH>(a, nb, s); return;
       default: break;
     }
   }
-  hipLaunchKernelGGL((gemm_bf16_8ph<L, E, OutT, true, 0, -1, NPH>), dim3(nb), dim3(512), 0, s, a);
+  launch_8ph_act<L, E, OutT, -1, NPH>(a, nb, s);
 }
 
 template <int L, int E>
@@ -1322,7 +1472,7 @@ static hipError_t dispatch_opt(int path, const GemmArgs& a, int in_dt, hipStream
     if (a.K % (2 * BT_K) == 0 && g_bf16_variant == 4)
       hipLaunchKernelGGL((gemm_bf16_8ph<L_TN, E, float, true, 0, -1, 4>), dim3(nb), dim3(512), 0, s, a);
     else if (a.K % (2 * BT_K) == 0 && g_bf16_variant != 1)
-      hipLaunchKernelGGL((gemm_bf16_8ph<L_TN, E, float, true>), dim3(nb), dim3(512), 0, s, a);
+      launch_8ph_act<L_TN, E, float, -1, 8>(a, nb, s);
     else
       hipLaunchKernelGGL((gemm_bf16_256<L_TN, E, float>), dim3(nb), dim3(512), 0, s, a);
     return hipGetLastError();
@@ -1358,6 +1508,7 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
   a.lr = lr; a.b1 = b1; a.b2 = b2; a.eps = eps; a.wd = wd; a.opt_m = opt_m; a.opt_v = opt_v;
   a.bc1 = 1.f; a.bc2 = 1.f;
   a.ksplit = 1;
+  a.tpb = 1;
   const bool opt_epi = (epi == EPI_SGD || epi == EPI_ADAM);
   if (opt_epi && (layout != L_TN || out_dtype != DT_F32)) return -1;
   if (epi == EPI_ADAM) {
@@ -1413,6 +1564,13 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
 int dllm_gemm_set_variant(int v) {
   const int old = g_bf16_variant;
   g_bf16_variant = v;
+  return old;
+}
+
+// tiles per persistent 8-phase block (<= 1: one block per tile); returns the previous value
+int dllm_gemm_set_tiles_per_block(int t) {
+  const int old = g_tpb;
+  g_tpb = t < 1 ? 1 : t;
   return old;
 }
 

@@ -245,6 +245,14 @@ def set_bf16_variant(name: str) -> str:
     return {v: k for k, v in BF16_VARIANTS.items()}[old]
 
 
+def set_tiles_per_block(n: int) -> int:
+    """Persistent 8-phase GEMM blocks (process-wide) for the FFN's own GEMMs: each block runs up to ``n``
+    output tiles back to back, the next tile's first K-tiles prefetched while the current tile's epilogue
+    runs (no pipeline drain or block relaunch per tile).  Capped at tiles / CUs so every CU keeps a block;
+    ``n <= 1``: one block per tile.  Default 2.  Returns the previous setting."""
+    return int(_native.lib().dllm_gemm_set_tiles_per_block(int(n)))
+
+
 def gemm_path(a_dtype: torch.dtype, out_dtype: torch.dtype, M: int, N: int, K: int,
               lda: int, ldb: int, ldc: int) -> str:
     """Which native kernel family a call would use: 'mfma_bf16', 'mfma_f32' or 'generic'."""

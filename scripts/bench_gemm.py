@@ -15,7 +15,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 import dllm  # noqa: E402,F401
-from dllm.ops.gemm import gemm, set_bf16_variant  # noqa: E402
+from dllm.ops.gemm import gemm, set_bf16_variant, set_tiles_per_block  # noqa: E402
 
 
 def timeit(fn, iters):
@@ -39,7 +39,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--group_m", type=int, default=4)
     ap.add_argument("--json", default="")
-    ap.add_argument("--variants", default="2stage,8phase,8phase_stagger")
+    ap.add_argument("--variants", default="2stage,8phase,8phase_stagger",
+                    help="main-loop variants; 'tpbN' = 8-phase staggered with N tiles per persistent block, "
+                         "'dyn' = dynamic persistent blocks")
     ap.add_argument("--cases", default="", help="comma-separated substrings selecting cases")
     ap.add_argument("--no_torch", action="store_true")
     a = ap.parse_args()
@@ -81,7 +83,12 @@ def main():
         tr = []
         for _ in range(a.rounds):  # interleaved rounds in one process (guide §5.4 rule 24)
             for v in variants:
-                set_bf16_variant(v)
+                if v.startswith("tpb"):
+                    set_bf16_variant("8phase_stagger")
+                    set_tiles_per_block(int(v[3:]))
+                else:
+                    set_bf16_variant(v)
+                    set_tiles_per_block(1)
                 times[v].append(timeit(mine, a.iters))
             tr.append(timeit(ref, a.iters))
         r = statistics.median(tr)
@@ -94,6 +101,7 @@ def main():
         res[name] = row
         print(msg, flush=True)
     set_bf16_variant("auto")
+    set_tiles_per_block(2)
     if a.json:
         with open(a.json, "w") as f:
             json.dump({"T": T, "D": D, "F": F, "cases": res}, f, indent=1)

@@ -272,3 +272,66 @@ def test_splitk_matches_unsplit(layout, epi):
     for x, y in zip(*res):
         tol = 2e-2 if x.dtype == torch.bfloat16 else 1e-5
         torch.testing.assert_close(x.float(), y.float(), rtol=tol, atol=tol * float(y.float().abs().max() + 1e-30))
+
+
+@pytest.mark.parametrize("tpb", [2, 3, 64])
+@pytest.mark.parametrize("layout,epi", [("nt", "act"), ("nt", "store"), ("nn", "dact"), ("nn", "store"),
+                                        ("tn", "sgd"), ("tn", "adam"), ("tn", "store_f32"), ("nt", "glu")])
+def test_persistent_blocks_bitwise_equal(tpb, layout, epi):
+    """Persistent 8-phase blocks (several tiles per block, next tile prefetched under the epilogue) give
+    bitwise the same results as one block per tile: same tiles, same K order, same epilogue."""
+    from dllm.ops.gemm import set_tiles_per_block
+
+    # 561 tiles: >= 2 per CU, so blocks run 2 tiles (288 blocks: 273 with two, 15 with one)
+    M, N, K = 4352, 8448, 384
+    a, b = _operands(layout, M, N, K, torch.bfloat16, seed=41)
+    a, b = a.cuda(), b.cuda()
+    res = []
+    for t in (1, tpb):
+        old = set_tiles_per_block(t)
+        try:
+            kw = {}
+            if epi in ("act", "store", "dact", "glu"):
+                out = torch.zeros(M, N // 2 if epi == "glu" else N, dtype=torch.bfloat16, device="cuda")
+                if epi == "act":
+                    kw = dict(epi="act", act="relu", aux_out=torch.zeros(M, N, dtype=torch.bfloat16, device="cuda"))
+                elif epi == "dact":
+                    kw = dict(epi="dact", act="gelu", aux=_mk((M, N), torch.bfloat16, 5).cuda())
+                elif epi == "glu":
+                    kw = dict(epi="glu", act="silu", aux_out=torch.zeros(M, N, dtype=torch.bfloat16, device="cuda"))
+            elif epi == "store_f32":
+                out = _mk((M, N), torch.float32, 8).cuda()
+                kw = dict(beta=1.0)
+            else:
+                out = _mk((M, N), torch.float32, 9).cuda()
+                kw = dict(epi=epi, lr=1e-3, aux_out=torch.zeros(M, N, dtype=torch.bfloat16, device="cuda"))
+                if epi == "adam":
+                    kw.update(step=2, opt_m=torch.full((M, N), 0.01, device="cuda"),
+                              opt_v=torch.full((M, N), 1e-4, device="cuda"))
+            gemm(a, b, layout, out=out, **kw)
+            torch.cuda.synchronize()
+            res.append([out] + [v for v in kw.values() if isinstance(v, torch.Tensor)])
+        finally:
+            set_tiles_per_block(old)
+    for x, y in zip(*res):
+        assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("layout", ["nt", "tn"])
+def test_persistent_blocks_splitk_bitwise_equal(layout):
+    """Persistent blocks over split-K slices (slot = tile x slice) == one block per slice, bitwise."""
+    from dllm.ops.gemm import choose_ksplit, set_tiles_per_block
+
+    M, N, K = 512, 512, 2048
+    assert choose_ksplit(M, N, K) > 1
+    a, b = _operands(layout, M, N, K, torch.bfloat16, seed=43)
+    a, b = a.cuda(), b.cuda()
+    outs = []
+    for t in (1, 2, 5):
+        old = set_tiles_per_block(t)
+        try:
+            outs.append(gemm(a, b, layout, out_dtype=torch.float32))
+            torch.cuda.synchronize()
+        finally:
+            set_tiles_per_block(old)
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
