@@ -88,6 +88,8 @@ def parse():
                    help="run the plain forward GEMM y = a·W2ᵀ (no epilogue) on hipBLASLt; all fused GEMMs stay native")
     p.add_argument("--tpb", type=int, default=0,
                    help="tiles per block of the 8-phase GEMM (persistent blocks; 0 = library default)")
+    p.add_argument("--no_relu_mask", action="store_true",
+                   help="ReLU dgrad reads the bf16 activation instead of the forward's 1-bit mask")
     p.add_argument("--force_comm", action="store_true",
                    help="exercise the RCCL DDP/FSDP path at N=1 (size-1 communicators, unfused optimizer)")
     return p.parse_args()
@@ -137,7 +139,8 @@ def main() -> int:
     cfg = TrainConfig(model=m, batch_size=a.batch_size, seq_len=a.seq_len, num_steps=a.steps, dtype=a.dtype,
                       grad_dtype=a.grad_dtype, optimizer=a.optimizer, dp_mode=dp_mode, dp=dp, tp=tp,
                       bucket_mb=a.bucket_mb, recompute=a.recompute, sequence_parallel=a.sequence_parallel,
-                      data="device", force_comm=a.force_comm, comm_backend=a.comm, side_optimizer=a.side_opt, tp_allreduce=a.tp_allreduce)
+                      data="device", force_comm=a.force_comm, comm_backend=a.comm, side_optimizer=a.side_opt, tp_allreduce=a.tp_allreduce,
+                      relu_mask=not a.no_relu_mask)
     mesh = Mesh.build(dp, tp, force=a.force_comm, comm_backend="torch" if cpu else a.comm,
                       device=None if cpu else dev)
     eng = FFNTrainer(cfg, mesh, dev)
@@ -204,7 +207,7 @@ def main() -> int:
         "tflops_per_gpu": round(tflops, 1), "mfu_dense": round(tflops / PEAK_TFLOPS[a.dtype], 4),
         "peak_hbm_gib": round(peak_gib, 2), "finite": finite, "comm": a.comm, "hip_graph": bool(a.graph),
         "plain_nt_gemm": "hipblaslt" if a.lib_plain_nt else "native", "gemm_variant": a.gemm_variant,
-        "gemm_tiles_per_block": a.tpb or "default",
+        "gemm_tiles_per_block": a.tpb or "default", "relu_mask": eng.masks is not None,
         "tp_allreduce": a.tp_allreduce,
     }
     if phases:

@@ -25,7 +25,8 @@ c_int, c_long, c_float, c_void_p, c_ull = ctypes.c_int, ctypes.c_long, ctypes.c_
 _SIGS = {
     "dllm_gemm": (c_int, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_long, c_void_p, c_long, c_void_p, c_long,
                           c_void_p, c_void_p, c_long, c_int, c_int, c_int, c_float, c_float, c_int, c_int, c_void_p,
-                          c_float, c_float, c_float, c_float, c_float, c_int, c_void_p, c_void_p, c_int, c_void_p]),
+                          c_float, c_float, c_float, c_float, c_float, c_int, c_void_p, c_void_p, c_int, c_void_p,
+                          c_void_p]),
     "dllm_gemm_path": (c_int, [c_int, c_int, c_int, c_int, c_int, c_long, c_long, c_long]),
     "dllm_rng_normal": (c_int, [c_void_p, c_int, c_long, c_ull, c_ull, c_float, c_void_p]),
     "dllm_rng_normal_devseed": (c_int, [c_void_p, c_int, c_long, c_void_p, c_ull, c_float, c_void_p]),

@@ -48,6 +48,10 @@ struct GemmArgs {
   int ksplit;
   // tiles per block of a persistent 8-phase kernel (PERS instantiations only)
   int tpb;
+  // ReLU activation-gradient bitmask (nullable; 8-phase kernels, bf16 out, compile-time ReLU): EPI_ACT writes
+  // bit (act(h) != 0) per output element, EPI_DACT reads it instead of aux.  Tile-native layout: 8 KiB per
+  // 256x256 tile (tile = tm * tiles_n + tn), 16 B per thread -- the same element->lane map in both GEMMs.
+  void* mask;
 };
 
 // ----------------------------------------------------------------------------------------------
@@ -295,6 +299,32 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
       for (int rg = 0; rg < 16; ++rg)
         store_rg(p.aux_out, p.ldaux, DLLM_M(rg), DLLM_NB(rg), DLLM_ACC(rg, 0), DLLM_ACC(rg, 1));
     }
+    if constexpr (ACT == ACT_RELU && BF) {
+      if (p.mask) {
+        // bit rg*8 + nt*4 + e of this thread's 128 = (stored bf16 activation != 0), i.e. exactly the
+        // act'(h) the unmasked dgrad derives from the stored activation
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int rg = 0; rg < 16; ++rg) {
+          f32x4_t a = DLLM_ACC(rg, 0), b = DLLM_ACC(rg, 1);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            a[e] = actf<ACT>(p.act, a[e]);
+            b[e] = actf<ACT>(p.act, b[e]);
+          }
+          const uint2 ua = pk_bf16(a), ub = pk_bf16(b);
+          const uint32_t bits = ((ua.x & 0xffffu) != 0u) | (((ua.x >> 16) != 0u) << 1) |
+                                (((ua.y & 0xffffu) != 0u) << 2) | (((ua.y >> 16) != 0u) << 3) |
+                                (((ub.x & 0xffffu) != 0u) << 4) | (((ub.x >> 16) != 0u) << 5) |
+                                (((ub.y & 0xffffu) != 0u) << 6) | (((ub.y >> 16) != 0u) << 7);
+          w[rg >> 2] |= bits << ((rg & 3) * 8);
+          *(uint4*)((uint16_t*)Cp + (long)DLLM_M(rg) * p.ldc + DLLM_NB(rg) + pc) = pair_swap(ua, ub);
+        }
+        const long tile = (long)(m0 / 256) * (p.N / 256) + n0 / 256;  // 256x256 tiles
+        ((uint4*)p.mask)[tile * 512 + (wr * 4 + wc) * 64 + lane] = uint4{w[0], w[1], w[2], w[3]};
+        return;
+      }
+    }
 #pragma unroll
     for (int rg = 0; rg < 16; ++rg) {
       f32x4_t a = DLLM_ACC(rg, 0), b = DLLM_ACC(rg, 1);
@@ -306,6 +336,25 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
       store_rg(Cp, p.ldc, DLLM_M(rg), DLLM_NB(rg), a, b);
     }
   } else if constexpr (EPI == EPI_DACT) {
+    if constexpr (ACT == ACT_RELU && BF) {
+      if (p.mask) {
+        const long tile = (long)(m0 / 256) * (p.N / 256) + n0 / 256;  // 256x256 tiles
+        const uint4 mv = ((const uint4*)p.mask)[tile * 512 + (wr * 4 + wc) * 64 + lane];
+        const uint32_t w[4] = {mv.x, mv.y, mv.z, mv.w};
+#pragma unroll
+        for (int rg = 0; rg < 16; ++rg) {
+          const uint32_t bits = w[rg >> 2] >> ((rg & 3) * 8);
+          f32x4_t a = DLLM_ACC(rg, 0), b = DLLM_ACC(rg, 1);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {  // multiply (not select): same -0 / NaN as the unmasked path
+            a[e] *= ((bits >> e) & 1u) ? 1.f : 0.f;
+            b[e] *= ((bits >> (4 + e)) & 1u) ? 1.f : 0.f;
+          }
+          store_rg(Cp, p.ldc, DLLM_M(rg), DLLM_NB(rg), a, b);
+        }
+        return;
+      }
+    }
 #pragma unroll
     for (int b0 = 0; b0 < 16; b0 += RB) {
       RT H[RB][2];
@@ -1496,7 +1545,7 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
               const void* B, long ldb, void* C, long ldc, const void* aux, void* aux_out, long ldaux,
               int M, int N, int K, float alpha, float beta, int group_m, int force_path, void* stream,
               float lr, float b1, float b2, float eps, float wd, int step, float* opt_m, float* opt_v,
-              int ksplit, float* workspace) {
+              int ksplit, float* workspace, void* mask) {
   if (M <= 0 || N <= 0 || K <= 0) return -1;
   if (layout < 0 || layout > 2) return -1;
   if ((epi == EPI_GLU || epi == EPI_DGLU) && (N % 32) != 0) return -1;
@@ -1509,6 +1558,7 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
   a.bc1 = 1.f; a.bc2 = 1.f;
   a.ksplit = 1;
   a.tpb = 1;
+  a.mask = nullptr;
   const bool opt_epi = (epi == EPI_SGD || epi == EPI_ADAM);
   if (opt_epi && (layout != L_TN || out_dtype != DT_F32)) return -1;
   if (epi == EPI_ADAM) {
@@ -1534,6 +1584,13 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
       a.ksplit = ksplit;
       g_splitk_ws = workspace;
     }
+  }
+  if (mask != nullptr) {
+    // the bitmask lives in the 8-phase kernels' tile-native layout: both GEMMs of a pair must run them
+    if ((epi != EPI_ACT && epi != EPI_DACT) || act != ACT_RELU || in_dtype != DT_BF16 || out_dtype != DT_BF16 ||
+        path != 0 || a.ksplit != 1 || K % (2 * BT_K) != 0 || g_bf16_variant == 1)
+      return -2;
+    a.mask = mask;
   }
   hipStream_t s = (hipStream_t)stream;
   hipError_t e;

@@ -94,13 +94,14 @@ def needs_preact(act: str, gated: bool) -> bool:
 
 def layer_fwd(x: torch.Tensor, w1: torch.Tensor, w2: torch.Tensor, act: str, gated: bool,
               a_out: torch.Tensor, h_out: torch.Tensor | None, y_out: torch.Tensor,
-              before_fwd2=None) -> torch.Tensor:
+              before_fwd2=None, mask: torch.Tensor | None = None) -> torch.Tensor:
     """y = act(x·W1ᵀ)·W2ᵀ  (gated: (act(x·W1ᵀ)⊙x·W3ᵀ)·W2ᵀ with ``w1`` = interleaved W13).
-    ``before_fwd2()`` runs between the two GEMMs (e.g. waiting for W2's all-gather)."""
+    ``before_fwd2()`` runs between the two GEMMs (e.g. waiting for W2's all-gather).  ``mask`` (ReLU):
+    the first GEMM also writes the activation-gradient bitmask the backward's dgrad reads."""
     if gated:
         gemm(x, w1, "nt", out=a_out, epi="glu", act=act, aux_out=h_out)
     else:
-        gemm(x, w1, "nt", out=a_out, epi="act", act=act, aux_out=h_out)
+        gemm(x, w1, "nt", out=a_out, epi="act", act=act, aux_out=h_out, mask=mask)
     if before_fwd2 is not None:
         before_fwd2()
     gemm(a_out, w2, "nt", out=y_out)
@@ -109,7 +110,7 @@ def layer_fwd(x: torch.Tensor, w1: torch.Tensor, w2: torch.Tensor, act: str, gat
 
 def layer_bwd(dy: torch.Tensor, x: torch.Tensor, w1: torch.Tensor, w2: torch.Tensor, act: str, gated: bool,
               a: torch.Tensor, h: torch.Tensor | None, gw1, gw2, da_buf: torch.Tensor,
-              dx_out: torch.Tensor | None, hooks=None) -> torch.Tensor | None:
+              dx_out: torch.Tensor | None, hooks=None, mask: torch.Tensor | None = None) -> torch.Tensor | None:
     """Backward of one layer; returns dx.
 
     ``gw1``/``gw2`` are either gradient tensors (overwritten) or dicts of ``gemm`` keyword arguments for the
@@ -124,7 +125,7 @@ def layer_bwd(dy: torch.Tensor, x: torch.Tensor, w1: torch.Tensor, w2: torch.Ten
     if gated:
         gemm(dy, w2, "nn", out=da_buf, epi="dglu", act=act, aux=h)    # [dg|du] interleaved [T, 2F]
     else:
-        gemm(dy, w2, "nn", out=da_buf, epi="dact", act=act, aux=h if h is not None else a)
+        gemm(dy, w2, "nn", out=da_buf, epi="dact", act=act, aux=h if h is not None else a, mask=mask)
     kw1 = gw1 if isinstance(gw1, dict) else {"out": gw1}
     kw2 = gw2 if isinstance(gw2, dict) else {"out": gw2}
     if dx_out is None:
@@ -152,9 +153,9 @@ def layer_bwd(dy: torch.Tensor, x: torch.Tensor, w1: torch.Tensor, w2: torch.Ten
 
 
 def recompute_fwd1(x: torch.Tensor, w1: torch.Tensor, act: str, gated: bool, a_out: torch.Tensor,
-                   h_out: torch.Tensor | None) -> None:
+                   h_out: torch.Tensor | None, mask: torch.Tensor | None = None) -> None:
     """Reference-style activation recompute (train_ffns.py:63,66) for ``recompute='full'``."""
     if gated:
         gemm(x, w1, "nt", out=a_out, epi="glu", act=act, aux_out=h_out)
     else:
-        gemm(x, w1, "nt", out=a_out, epi="act", act=act, aux_out=h_out)
+        gemm(x, w1, "nt", out=a_out, epi="act", act=act, aux_out=h_out, mask=mask)

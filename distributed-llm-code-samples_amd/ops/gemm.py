@@ -159,6 +159,7 @@ def set_splitk(enabled: bool) -> bool:
 
 
 _LIBRARY_PLAIN_NT = {"enabled": False}
+_VARIANT = {"name": "auto"}
 
 
 def set_library_plain_nt(enabled: bool) -> bool:
@@ -175,7 +176,10 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
          alpha: float = 1.0, beta: float = 0.0, out_dtype: torch.dtype | None = None, group_m: int = 4,
          force: str | None = None, lr: float = 0.0, betas: tuple = (0.9, 0.95), eps: float = 1e-8,
          wd: float = 0.0, step: int = 0, opt_m: torch.Tensor | None = None,
-         opt_v: torch.Tensor | None = None) -> torch.Tensor:
+         opt_v: torch.Tensor | None = None, mask: torch.Tensor | None = None) -> torch.Tensor:
+    """``mask`` (ReLU only, GPU, see ``relu_mask_supported``): ``epi="act"`` also writes the activation-gradient
+    bitmask, ``epi="dact"`` reads it instead of ``aux`` (1 bit instead of a bf16 per element).  CPU tensors
+    ignore it (``aux`` stays the source of truth there)."""
     M, N, K = gemm_shape(a, b, layout)
     if a.dtype != b.dtype:
         raise TypeError(f"gemm operands differ in dtype: {a.dtype} vs {b.dtype}")
@@ -231,9 +235,28 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
                      _native.stream_ptr(a.device), float(lr), float(betas[0]), float(betas[1]), float(eps),
                      float(wd), int(step), opt_m.data_ptr() if opt_m is not None else None,
                      opt_v.data_ptr() if opt_v is not None else None, ksplit,
-                     ws.data_ptr() if ws is not None else None)
+                     ws.data_ptr() if ws is not None else None,
+                     _mask_ptr(mask, M, N) if mask is not None else None)
     _native.check(rc, f"dllm_gemm({layout},{epi},M={M},N={N},K={K})")
     return out
+
+
+def relu_mask_bytes(M: int, N: int) -> int:
+    """Size of the ReLU bitmask of an ``[M, N]`` activation (8 KiB per 256x256 tile)."""
+    return (M // 256) * (N // 256) * 8192
+
+
+def relu_mask_supported(M: int, N: int, K: int, dtype: torch.dtype = torch.bfloat16) -> bool:
+    """Whether the forward (``x·W1ᵀ``, K = D) / dgrad (``dy·W2``, K = D) pair of an ``[M, N]`` ReLU activation runs
+    on the 8-phase kernels that share the bitmask's tile-native layout."""
+    return (dtype == torch.bfloat16 and M % 256 == 0 and N % 256 == 0 and K % 128 == 0
+            and choose_ksplit(M, N, K) == 1 and _VARIANT["name"] != "2stage")
+
+
+def _mask_ptr(mask: torch.Tensor, M: int, N: int) -> int:
+    if mask.dtype != torch.uint8 or not mask.is_contiguous() or mask.numel() < relu_mask_bytes(M, N):
+        raise ValueError(f"ReLU mask must be a contiguous uint8 buffer of >= {relu_mask_bytes(M, N)} bytes")
+    return mask.data_ptr()
 
 
 BF16_VARIANTS = {"auto": 0, "2stage": 1, "8phase": 2, "8phase_stagger": 3, "4phase_stagger": 4}
@@ -242,6 +265,7 @@ BF16_VARIANTS = {"auto": 0, "2stage": 1, "8phase": 2, "8phase_stagger": 3, "4pha
 def set_bf16_variant(name: str) -> str:
     """Select the bf16 256x256 main loop (process-wide); returns the previous setting's name."""
     old = _native.lib().dllm_gemm_set_variant(BF16_VARIANTS[name])
+    _VARIANT["name"] = name
     return {v: k for k, v in BF16_VARIANTS.items()}[old]
 
 

@@ -195,6 +195,14 @@ class FFNTrainer:
         self.acts_h = ([torch.empty((T, self.R1), dtype=self.cd, device=dev) for _ in range(nA)]
                        if self.need_h else None)
         self.da = torch.empty((T, self.R1), dtype=self.cd, device=dev)
+        # ReLU: 1-bit activation-gradient masks (written by the forward's first GEMM, read by the dgrad)
+        self.masks = None
+        if cfg.relu_mask and self.act == "relu" and not self.gated and dev.type == "cuda":
+            from ..ops.gemm import relu_mask_bytes, relu_mask_supported
+
+            if relu_mask_supported(T, self.F_loc, D, self.cd):
+                self.masks = [torch.empty(relu_mask_bytes(T, self.F_loc), dtype=torch.uint8, device=dev)
+                              for _ in range(nA)]
         self.dxb = [torch.empty((T, D), dtype=self.cd, device=dev) for _ in range(2)]
         if self.sp:
             self.xfull = torch.empty((T, D), dtype=self.cd, device=dev)       # gathered layer input
@@ -251,6 +259,11 @@ class FFNTrainer:
 
     def grad_view(self, l: int, name: str) -> torch.Tensor:
         return self._view(self.grads, self.entry[(l, name)])
+
+    def _mask(self, l: int) -> torch.Tensor | None:
+        if self.masks is None:
+            return None
+        return self.masks[l if self.cfg.recompute == "none" else 0]
 
     def layer_order(self, l: int) -> tuple[str, str]:
         """Order in which layer l's weight gradients complete in the backward (= flat layout order)."""
@@ -553,7 +566,7 @@ class FFNTrainer:
                     self._ddp_wait(l, "w2")
                 xin = self.xs_full[l] if keep else self.xfull
                 comm.all_gather_into(xin, self.xs[l], tpg, async_op=True).wait()
-                layer_fwd(xin, w1, w2, act, gated, a, h, self.yfull)
+                layer_fwd(xin, w1, w2, act, gated, a, h, self.yfull, mask=self._mask(l))
                 comm.reduce_scatter_into(self.xs[l + 1], self.yfull, tpg, async_op=True).wait()
             else:
                 before2 = None
@@ -567,7 +580,8 @@ class FFNTrainer:
                 elif self.ddp:
                     def before2(l=l):
                         self._ddp_wait(l, "w2")
-                layer_fwd(self.xs[l], w1, w2, act, gated, a, h, self.xs[l + 1], before_fwd2=before2)
+                layer_fwd(self.xs[l], w1, w2, act, gated, a, h, self.xs[l + 1], before_fwd2=before2,
+                          mask=self._mask(l))
                 if self.tp_car is not None:
                     self.tp_car.all_reduce(self.xs[l + 1])
                 elif self.mesh.tp > 1:
@@ -614,19 +628,19 @@ class FFNTrainer:
                 xin = self.xs_full[l] if keep else self.xfull
                 if not keep:
                     comm.all_gather_into(xin, self.xs[l], tpg, async_op=True).wait()
-                    recompute_fwd1(xin, w1, act, gated, a, h)
+                    recompute_fwd1(xin, w1, act, gated, a, h, mask=self._mask(l))
                 hooks_sp = _SPHooks(self, l)
                 dxp = layer_bwd(self.dyfull, xin, w1, w2, act, gated, a, h, gw1, gw2, self.da,
-                                self.dxb[l % 2] if need_dx else None, hooks_sp)
+                                self.dxb[l % 2] if need_dx else None, hooks_sp, mask=self._mask(l))
                 if dxp is not None:
                     out = self.dxs[l % 2]
                     comm.reduce_scatter_into(out, dxp, tpg, async_op=True).wait()
                     g = out
             else:
                 if not keep:
-                    recompute_fwd1(self.xs[l], w1, act, gated, a, h)
+                    recompute_fwd1(self.xs[l], w1, act, gated, a, h, mask=self._mask(l))
                 dx = layer_bwd(g, self.xs[l], w1, w2, act, gated, a, h, gw1, gw2, self.da,
-                               self.dxb[l % 2] if need_dx else None, hooks)
+                               self.dxb[l % 2] if need_dx else None, hooks, mask=self._mask(l))
                 if dx is not None:
                     g = dx
             if self.zero:

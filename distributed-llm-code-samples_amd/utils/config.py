@@ -64,6 +64,8 @@ class TrainConfig:
     skip_input_grad: bool = True     # layer-0 dx is never consumed (reference computes it, :68)
     separate_streams: bool = True    # one communicator/stream per comm role
     tp_overlap: bool = True          # overlap the TP dx all-reduce with the dW1 GEMM
+    relu_mask: bool = True           # ReLU: the dgrad reads a 1-bit activation mask written by the forward
+                                     # GEMM instead of the bf16 activation (GPU, 8-phase kernel shapes)
     fused_optimizer: bool = True     # fuse SGD/Adam into the wgrad GEMM epilogue when no grad collective
     side_optimizer: int = 0          # >0 (no grad collective, SGD): wgrad GEMMs store grads and a side stream
                                      # applies SGD on this many workgroups, overlapped with the next GEMMs

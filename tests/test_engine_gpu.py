@@ -174,3 +174,21 @@ def test_odd_shapes_and_skipped_input_grad(dtype):
             d_got, d_want = g[k].double() - p0[k].double(), w[k].double() - p0[k].double()
             rel = (d_got - d_want).norm() / d_want.norm()
             assert rel < (2e-3 if dtype == "fp32" else 2e-2), (k, rel.item())
+
+
+def test_relu_mask_engine_bitwise():
+    """A bf16 ReLU training step with the 1-bit activation masks == the same step reading the activations."""
+    D, F, L, T, lr = 512, 2048, 3, 1024, 1e-2
+    layers, batches = _setup(D, F, L, T, "relu", False, 2)
+    outs = []
+    for use in (False, True):
+        cfg = TrainConfig(model=ModelConfig(D, F, L, "relu", False), batch_size=1, seq_len=T, dtype="bf16",
+                          grad_dtype="fp32", lr=lr, relu_mask=use)
+        eng = FFNTrainer(cfg, Mesh(), torch.device("cuda"))
+        assert (eng.masks is not None) == use
+        eng.load_full_params(layers)
+        for x, dy in batches:
+            eng.train_step(x.cuda().bfloat16(), dy.cuda().bfloat16())
+        torch.cuda.synchronize()
+        outs.append(eng.master.clone())
+    assert torch.equal(outs[0], outs[1])

@@ -335,3 +335,44 @@ def test_persistent_blocks_splitk_bitwise_equal(layout):
         finally:
             set_tiles_per_block(old)
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+
+
+@pytest.mark.parametrize("tpb", [1, 2])
+def test_relu_mask_matches_activation_path(tpb):
+    """ReLU bitmask written by the forward GEMM and read by the dgrad == dgrad masked by the stored
+    activation, bitwise (incl. -0 for negative masked values); forward output unchanged."""
+    from dllm.ops.gemm import relu_mask_bytes, relu_mask_supported, set_tiles_per_block
+
+    M, F, D = 4608, 2304, 512   # 162 tiles: one / two per block
+    assert relu_mask_supported(M, F, D)
+    x, w1 = _operands("nt", M, F, D, torch.bfloat16, seed=51)
+    dy, w2 = _operands("nn", M, F, D, torch.bfloat16, seed=52)
+    x, w1, dy, w2 = x.cuda(), w1.cuda(), dy.cuda(), w2.cuda()
+    old = set_tiles_per_block(tpb)
+    try:
+        a0 = torch.empty(M, F, dtype=torch.bfloat16, device="cuda")
+        gemm(x, w1, "nt", out=a0, epi="act", act="relu")
+        da0 = torch.empty(M, F, dtype=torch.bfloat16, device="cuda")
+        gemm(dy, w2, "nn", out=da0, epi="dact", act="relu", aux=a0)
+        mask = torch.full((relu_mask_bytes(M, F),), 0xA5, dtype=torch.uint8, device="cuda")
+        a1 = torch.empty_like(a0)
+        gemm(x, w1, "nt", out=a1, epi="act", act="relu", mask=mask)
+        da1 = torch.empty_like(da0)
+        gemm(dy, w2, "nn", out=da1, epi="dact", act="relu", aux=a1, mask=mask)
+        torch.cuda.synchronize()
+    finally:
+        set_tiles_per_block(old)
+    assert torch.equal(a0.view(torch.int16), a1.view(torch.int16))
+    assert torch.equal(da0.view(torch.int16), da1.view(torch.int16))
+    frac = (a1 != 0).float().mean().item()
+    assert 0.3 < frac < 0.7  # the mask really masks
+
+
+def test_relu_mask_rejected_off_the_8phase_path():
+    from dllm.ops.gemm import relu_mask_bytes
+
+    M, N, K = 512, 512, 192   # K % 128 != 0 -> 2-stage kernel: no tile-native mask layout
+    x, w = _operands("nt", M, N, K, torch.bfloat16, seed=1)
+    mask = torch.empty(relu_mask_bytes(M, N), dtype=torch.uint8, device="cuda")
+    with pytest.raises(RuntimeError):
+        gemm(x.cuda(), w.cuda(), "nt", out_dtype=torch.bfloat16, epi="act", act="relu", mask=mask)
