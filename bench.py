@@ -83,11 +83,11 @@ def parse():
                    help="TP activation all-reduce: RCCL, or the custom two-shot xGMI peer all-reduce (csrc/car.hip)")
     p.add_argument("--gemm_variant", default="auto",
                    choices=["auto", "2stage", "8phase", "8phase_stagger", "4phase_stagger"],
-                   help="bf16 GEMM main-loop schedule (auto = 4-phase staggered when K % 128 == 0)")
+                   help="bf16 GEMM main-loop schedule (auto = 8-phase staggered when K % 128 == 0)")
     p.add_argument("--lib_plain_nt", action="store_true",
                    help="run the plain forward GEMM y = a·W2ᵀ (no epilogue) on hipBLASLt; all fused GEMMs stay native")
     p.add_argument("--tpb", type=int, default=0,
-                   help="tiles per block of the 8-phase GEMM (persistent blocks; 0 = library default)")
+                   help="tiles per persistent 8-phase GEMM block (0 = auto: 2, or 1 for gated stacks; 1 = off)")
     p.add_argument("--no_relu_mask", action="store_true",
                    help="ReLU dgrad reads the bf16 activation instead of the forward's 1-bit mask")
     p.add_argument("--force_comm", action="store_true",
@@ -127,10 +127,6 @@ def main() -> int:
         from dllm.ops.gemm import set_bf16_variant
 
         set_bf16_variant(a.gemm_variant)
-    if a.tpb and not cpu:
-        from dllm.ops.gemm import set_tiles_per_block
-
-        set_tiles_per_block(a.tpb)
     if a.lib_plain_nt:
         from dllm.ops.gemm import set_library_plain_nt
 
@@ -140,7 +136,7 @@ def main() -> int:
                       grad_dtype=a.grad_dtype, optimizer=a.optimizer, dp_mode=dp_mode, dp=dp, tp=tp,
                       bucket_mb=a.bucket_mb, recompute=a.recompute, sequence_parallel=a.sequence_parallel,
                       data="device", force_comm=a.force_comm, comm_backend=a.comm, side_optimizer=a.side_opt, tp_allreduce=a.tp_allreduce,
-                      relu_mask=not a.no_relu_mask)
+                      relu_mask=not a.no_relu_mask, gemm_tiles_per_block=a.tpb)
     mesh = Mesh.build(dp, tp, force=a.force_comm, comm_backend="torch" if cpu else a.comm,
                       device=None if cpu else dev)
     eng = FFNTrainer(cfg, mesh, dev)
@@ -207,7 +203,7 @@ def main() -> int:
         "tflops_per_gpu": round(tflops, 1), "mfu_dense": round(tflops / PEAK_TFLOPS[a.dtype], 4),
         "peak_hbm_gib": round(peak_gib, 2), "finite": finite, "comm": a.comm, "hip_graph": bool(a.graph),
         "plain_nt_gemm": "hipblaslt" if a.lib_plain_nt else "native", "gemm_variant": a.gemm_variant,
-        "gemm_tiles_per_block": a.tpb or "default", "relu_mask": eng.masks is not None,
+        "gemm_tiles_per_block": a.tpb or ("auto: 1" if m.gated else "auto: 2"), "relu_mask": eng.masks is not None,
         "tp_allreduce": a.tp_allreduce,
     }
     if phases:

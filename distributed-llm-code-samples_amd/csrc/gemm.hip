@@ -300,30 +300,35 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
         store_rg(p.aux_out, p.ldaux, DLLM_M(rg), DLLM_NB(rg), DLLM_ACC(rg, 0), DLLM_ACC(rg, 1));
     }
     if constexpr (ACT == ACT_RELU && BF) {
-      if (p.mask) {
-        // bit rg*8 + nt*4 + e of this thread's 128 = (stored bf16 activation != 0), i.e. exactly the
-        // act'(h) the unmasked dgrad derives from the stored activation
-        uint32_t w[4] = {0u, 0u, 0u, 0u};
+      // optional mask: bit rg*8 + nt*4 + e of this thread's 128 = (stored bf16 activation != 0), i.e. exactly
+      // the act'(h) the unmasked dgrad derives from the stored activation; one dword per 4 row groups
+      const bool mk = p.mask != nullptr;
+      const long tile = (long)(m0 / 256) * (p.N / 256) + n0 / 256;  // 256x256 tiles
+      uint32_t* mw = (uint32_t*)p.mask + (tile * 512 + (wr * 4 + wc) * 64 + lane) * 4;
+      uint32_t w = 0u;
 #pragma unroll
-        for (int rg = 0; rg < 16; ++rg) {
-          f32x4_t a = DLLM_ACC(rg, 0), b = DLLM_ACC(rg, 1);
+      for (int rg = 0; rg < 16; ++rg) {
+        f32x4_t a = DLLM_ACC(rg, 0), b = DLLM_ACC(rg, 1);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            a[e] = actf<ACT>(p.act, a[e]);
-            b[e] = actf<ACT>(p.act, b[e]);
-          }
-          const uint2 ua = pk_bf16(a), ub = pk_bf16(b);
+        for (int e = 0; e < 4; ++e) {
+          a[e] = actf<ACT>(p.act, a[e]);
+          b[e] = actf<ACT>(p.act, b[e]);
+        }
+        const uint2 ua = pk_bf16(a), ub = pk_bf16(b);
+        *(uint4*)((uint16_t*)Cp + (long)DLLM_M(rg) * p.ldc + DLLM_NB(rg) + pc) = pair_swap(ua, ub);
+        if (mk) {
           const uint32_t bits = ((ua.x & 0xffffu) != 0u) | (((ua.x >> 16) != 0u) << 1) |
                                 (((ua.y & 0xffffu) != 0u) << 2) | (((ua.y >> 16) != 0u) << 3) |
                                 (((ub.x & 0xffffu) != 0u) << 4) | (((ub.x >> 16) != 0u) << 5) |
                                 (((ub.y & 0xffffu) != 0u) << 6) | (((ub.y >> 16) != 0u) << 7);
-          w[rg >> 2] |= bits << ((rg & 3) * 8);
-          *(uint4*)((uint16_t*)Cp + (long)DLLM_M(rg) * p.ldc + DLLM_NB(rg) + pc) = pair_swap(ua, ub);
+          w |= bits << ((rg & 3) * 8);
+          if ((rg & 3) == 3) {
+            mw[rg >> 2] = w;
+            w = 0u;
+          }
         }
-        const long tile = (long)(m0 / 256) * (p.N / 256) + n0 / 256;  // 256x256 tiles
-        ((uint4*)p.mask)[tile * 512 + (wr * 4 + wc) * 64 + lane] = uint4{w[0], w[1], w[2], w[3]};
-        return;
       }
+      return;
     }
 #pragma unroll
     for (int rg = 0; rg < 16; ++rg) {
@@ -665,22 +670,25 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_256(GemmArgs p) {
 // ----------------------------------------------------------------------------------------------
 constexpr int HT = 16384;  // half-tile bytes
 
-__device__ __forceinline__ void kc_half_offsets(long ld, int wid, int lane, long off[2]) {
+// Per-lane BYTE offsets (32-bit) of the 8-phase kernel's LDS-DMA pieces: with a uniform 64-bit panel base
+// they select the SGPR-base + 32-bit VGPR-offset addressing form (no per-stage 64-bit VALU adds, half the
+// VGPRs a 64-bit offset pair costs).
+__device__ __forceinline__ void kc_half_offsets(long ld, int wid, int lane, uint32_t off[2]) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int q = wid + 8 * i;  // piece 0..15: rows 8q..8q+7
     const int row = 8 * q + (lane >> 3);
     const int c = (lane & 7) ^ ((row >> 1) & 7);
-    off[i] = (long)row * ld + c * 8;
+    off[i] = (uint32_t)(((long)row * ld + c * 8) * 2);
   }
 }
-__device__ __forceinline__ void mc_half_offsets(long ld, int wid, int lane, long off[2]) {
+__device__ __forceinline__ void mc_half_offsets(long ld, int wid, int lane, uint32_t off[2]) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int q = wid + 8 * i;  // piece 0..15: k rows 4q..4q+3 of 256 B
     const int krow = 4 * q + (lane >> 4);
     const int u = (lane & 15) >> 1, h = lane & 1;
-    off[i] = (long)krow * ld + ((u ^ mc_swz(krow)) * 16) + h * 8;
+    off[i] = (uint32_t)(((long)krow * ld + ((u ^ mc_swz(krow)) * 16) + h * 8) * 2);
   }
 }
 // MN-contiguous half-tile fragment: rows of 256 B, 8 units of 32 B, unit XOR mc_swz(k) (3 bits)
@@ -787,7 +795,7 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
   constexpr bool B_KC = (ABL & 2) ? true : (LAYOUT == L_NT);
   constexpr bool A_RKC = (ABL & 4) ? true : (LAYOUT != L_TN);
   constexpr bool B_RKC = (ABL & 8) ? true : (LAYOUT == L_NT);
-  long aoff[2], boff[2];
+  uint32_t aoff[2], boff[2];
   if constexpr (A_KC) kc_half_offsets(p.lda, wid, lane, aoff); else mc_half_offsets(p.lda, wid, lane, aoff);
   if constexpr (B_KC) kc_half_offsets(p.ldb, wid, lane, boff); else mc_half_offsets(p.ldb, wid, lane, boff);
   const long a_kstep = A_KC ? BT_K : (long)BT_K * p.lda;
@@ -825,9 +833,9 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
   auto stage_at = [&](int op, int hh, const uint16_t* src, int buf) {
     DLLM_LDS char* dst = lds + ((op * 2 + hh) * 2 + buf) * HT;
     src += op == 0 ? hh * a_hstep : hh * b_hstep;
-    const long* off = op == 0 ? aoff : boff;
-    glds16(src + off[0], dst + wid * 1024);
-    glds16(src + off[1], dst + (wid + 8) * 1024);
+    const uint32_t* off = op == 0 ? aoff : boff;
+    glds16((const uint16_t*)((const char*)src + off[0]), dst + wid * 1024);
+    glds16((const uint16_t*)((const char*)src + off[1]), dst + (wid + 8) * 1024);
   };
   // 8-phase loop: running prefetch pointers at K-tile 2*it + 2 of the current slot; in the final iteration
   // they move to the NEXT slot's K-tile 0, so the last iteration's prefetches (K-tiles "nk", "nk+1") are
@@ -1412,20 +1420,21 @@ static float* g_splitk_ws = nullptr;  // set per call by dllm_gemm (caller-owned
 
 // staggered 8-phase launch; the FFN's own activation epilogues (NT act/glu forward, NN dact/dglu
 // dgrad, bf16 out) get a compile-time activation, everything else the runtime switch
-// persistent instantiations exist for the FFN's own GEMMs only: bf16-out forward / dgrad GEMMs with a
-// compile-time activation (or none), and the weight-gradient GEMMs (stored gradients, fused optimizers)
-template <int L, int E, typename OutT>
+// Persistent instantiations exist where they measured faster end to end (profiles/persistent_blocks_r1.log):
+// the ReLU FFN's GEMMs -- bf16 forward / dgrad with a compile-time ReLU epilogue or a plain store -- and the
+// weight-gradient GEMMs (stored gradients, fused SGD).  Gated (GLU/DGLU), SiLU/GELU and fused-AdamW epilogues
+// stay one tile per block: their heavier in-loop epilogues measured 2 % slower persistent.
+template <int L, int E, typename OutT, int ACT>
 constexpr bool persistent_kernel() {
   constexpr bool bf = std::is_same<OutT, uint16_t>::value;
-  if constexpr (L == L_NT) return bf && (E == EPI_ACT || E == EPI_GLU || E == EPI_STORE);
-  if constexpr (L == L_NN) return bf && (E == EPI_DACT || E == EPI_DGLU || E == EPI_STORE);
-  return E == EPI_STORE || E == EPI_SGD || E == EPI_ADAM;
+  if constexpr (L == L_NT) return bf && ((E == EPI_ACT && ACT == ACT_RELU) || E == EPI_STORE);
+  if constexpr (L == L_NN) return bf && ((E == EPI_DACT && ACT == ACT_RELU) || E == EPI_STORE);
+  return E == EPI_STORE || E == EPI_SGD;
 }
 
 template <int L, int E, typename OutT, int ACT, int NPH>
 static void launch_8ph_act(const GemmArgs& a0, int nb0, hipStream_t s) {
-  if constexpr (NPH == 8 && persistent_kernel<L, E, OutT>() && (ACT >= 0 || !(E == EPI_ACT || E == EPI_GLU ||
-                                                                                 E == EPI_DACT || E == EPI_DGLU))) {
+  if constexpr (NPH == 8 && persistent_kernel<L, E, OutT, ACT>()) {
     GemmArgs a = a0;
     const int nb = grid_8ph(a, nb0);
     if (a.tpb > 1) {

@@ -125,6 +125,10 @@ class FFNTrainer:
         self.T = T
         self.step_count = 0
         dev = self.device
+        if dev.type == "cuda":
+            from ..ops.gemm import set_tiles_per_block
+
+            set_tiles_per_block(cfg.gemm_tiles_per_block or (1 if m.gated else 2))
         if cfg.debug_sync:
             comm.set_serialize(True)
         # custom xGMI all-reduce for the TP activation exchange (opt-in; gradients stay on RCCL)

@@ -295,8 +295,8 @@ def test_persistent_blocks_bitwise_equal(tpb, layout, epi):
                 out = torch.zeros(M, N // 2 if epi == "glu" else N, dtype=torch.bfloat16, device="cuda")
                 if epi == "act":
                     kw = dict(epi="act", act="relu", aux_out=torch.zeros(M, N, dtype=torch.bfloat16, device="cuda"))
-                elif epi == "dact":
-                    kw = dict(epi="dact", act="gelu", aux=_mk((M, N), torch.bfloat16, 5).cuda())
+                elif epi == "dact":   # ReLU: the persistent instantiation
+                    kw = dict(epi="dact", act="relu", aux=_mk((M, N), torch.bfloat16, 5).cuda())
                 elif epi == "glu":
                     kw = dict(epi="glu", act="silu", aux_out=torch.zeros(M, N, dtype=torch.bfloat16, device="cuda"))
             elif epi == "store_f32":
