@@ -376,3 +376,23 @@ def test_relu_mask_rejected_off_the_8phase_path():
     mask = torch.empty(relu_mask_bytes(M, N), dtype=torch.uint8, device="cuda")
     with pytest.raises(RuntimeError):
         gemm(x.cuda(), w.cuda(), "nt", out_dtype=torch.bfloat16, epi="act", act="relu", mask=mask)
+
+
+@pytest.mark.parametrize("layout,M,N,K", [("nt", 4352, 8448, 384), ("nn", 2048, 4096, 1024), ("tn", 2560, 3072, 2048),
+                                          ("tn", 512, 512, 2048)])
+def test_race_screen_repeated_runs_bitwise(layout, M, N, K):
+    """Kernel race screen (cdna_hip_programming.md §5 race screens): the LDS-DMA pipeline, the staggered
+    barriers and the persistent slot loop must give bitwise-identical results on every run, with random data,
+    across persistent (> 2 tiles / CU), one-tile and split-K grids."""
+    a, b = _operands(layout, M, N, K, torch.bfloat16, seed=M + K)
+    a, b = a.cuda(), b.cuda()
+    first = gemm(a, b, layout, out_dtype=torch.float32)
+    outs = [torch.empty_like(first) for _ in range(12)]
+    for o in outs:
+        gemm(a, b, layout, out=o)
+    torch.cuda.synchronize()
+    for o in outs:
+        assert torch.equal(o, first)
+    ref = _ref(a[:256].cpu() if layout != "tn" else a[:, :256].cpu(), b.cpu(), layout)
+    got = first[:256].cpu().double()
+    assert ((got - ref).abs().max() / ref.abs().max()) < 1e-5
