@@ -88,6 +88,8 @@ def parse():
                    help="run the plain forward GEMM y = a·W2ᵀ (no epilogue) on hipBLASLt; all fused GEMMs stay native")
     p.add_argument("--tpb", type=int, default=0,
                    help="tiles per persistent 8-phase GEMM block (0 = auto: 2, or 1 for gated stacks; 1 = off)")
+    p.add_argument("--wgrad_stream", action="store_true",
+                   help="N=1: weight-gradient GEMMs (fused SGD) on a second stream, concurrent with the dgrads")
     p.add_argument("--no_relu_mask", action="store_true",
                    help="ReLU dgrad reads the bf16 activation instead of the forward's 1-bit mask")
     p.add_argument("--force_comm", action="store_true",
@@ -136,7 +138,8 @@ def main() -> int:
                       grad_dtype=a.grad_dtype, optimizer=a.optimizer, dp_mode=dp_mode, dp=dp, tp=tp,
                       bucket_mb=a.bucket_mb, recompute=a.recompute, sequence_parallel=a.sequence_parallel,
                       data="device", force_comm=a.force_comm, comm_backend=a.comm, side_optimizer=a.side_opt, tp_allreduce=a.tp_allreduce,
-                      relu_mask=not a.no_relu_mask, gemm_tiles_per_block=a.tpb)
+                      relu_mask=not a.no_relu_mask, gemm_tiles_per_block=a.tpb,
+                      wgrad_stream=a.wgrad_stream)
     mesh = Mesh.build(dp, tp, force=a.force_comm, comm_backend="torch" if cpu else a.comm,
                       device=None if cpu else dev)
     eng = FFNTrainer(cfg, mesh, dev)
@@ -204,6 +207,7 @@ def main() -> int:
         "peak_hbm_gib": round(peak_gib, 2), "finite": finite, "comm": a.comm, "hip_graph": bool(a.graph),
         "plain_nt_gemm": "hipblaslt" if a.lib_plain_nt else "native", "gemm_variant": a.gemm_variant,
         "gemm_tiles_per_block": a.tpb or ("auto: 1" if m.gated else "auto: 2"), "relu_mask": eng.masks is not None,
+        "wgrad_stream": eng.wg_stream is not None,
         "tp_allreduce": a.tp_allreduce,
     }
     if phases:

@@ -207,7 +207,19 @@ class FFNTrainer:
             if relu_mask_supported(T, self.F_loc, D, self.cd):
                 self.masks = [torch.empty(relu_mask_bytes(T, self.F_loc), dtype=torch.uint8, device=dev)
                               for _ in range(nA)]
-        self.dxb = [torch.empty((T, D), dtype=self.cd, device=dev) for _ in range(2)]
+        # concurrent weight-gradient stream (single device, fused optimizer, kept activations): the dgrad
+        # chain (da, dx) stays on the compute stream, dW2 / dW1 run on a side stream after the dgrad that
+        # last reads the weight they update; da / dx buffers rotate so the side stream's reads never race
+        # the next layers' writes
+        self.wg_stream = None
+        if (cfg.wgrad_stream and self.fused_opt and dev.type == "cuda" and t == 1 and not self.sp
+                and cfg.recompute == "none"):
+            self.wg_stream = torch.cuda.Stream(device=dev)
+            self.da_ring = [self.da, torch.empty_like(self.da)]
+            self.da_free = [None, None]
+            self.dx_free = [None, None, None]
+        self.dxb = [torch.empty((T, D), dtype=self.cd, device=dev)
+                    for _ in range(3 if self.wg_stream is not None else 2)]
         if self.sp:
             self.xfull = torch.empty((T, D), dtype=self.cd, device=dev)       # gathered layer input
             self.yfull = torch.empty((T, D), dtype=self.cd, device=dev)       # partial output
@@ -263,6 +275,43 @@ class FFNTrainer:
 
     def grad_view(self, l: int, name: str) -> torch.Tensor:
         return self._view(self.grads, self.entry[(l, name)])
+
+    def _layer_bwd_concurrent(self, l, g, w1, w2, a, h, kw1, kw2, need_dx):
+        """One layer's backward with the weight-gradient GEMMs on ``wg_stream`` (same math and order per
+        stream as ``layer_bwd``).  Edges: dW2 after da (da reads the W2 copy dW2's fused update rewrites),
+        dW1 after dx (same for W1); buffers are reused only after the side stream's last read of them."""
+        from ..ops.gemm import gemm
+
+        main, side = torch.cuda.current_stream(self.device), self.wg_stream
+        act = self.act
+        da = self.da_ring[l % 2]
+        if self.da_free[l % 2] is not None:
+            main.wait_event(self.da_free[l % 2])
+        gemm(g, w2, "nn", out=da, epi="dact", act=act, aux=h if h is not None else a, mask=self._mask(l))
+        e_da = torch.cuda.Event()
+        e_da.record(main)
+        side.wait_event(e_da)
+        if need_dx:
+            with torch.cuda.stream(side):
+                gemm(g, a, "tn", **kw2)                                   # dW2 = dyᵀ·a
+                e_dy = torch.cuda.Event()
+                e_dy.record(side)
+            j = l % 3
+            if self.dx_free[j] is not None:
+                main.wait_event(self.dx_free[j])
+            dx = gemm(da, w1, "nn", out=self.dxb[j])                     # dx = da·W1
+            self.dx_free[(l + 1) % 3] = e_dy                              # g (= dx of layer l+1) read
+            e_dx = torch.cuda.Event()
+            e_dx.record(main)
+            side.wait_event(e_dx)
+        with torch.cuda.stream(side):
+            gemm(da, self.xs[l], "tn", **kw1)                             # dW1 = daᵀ·x
+            if not need_dx:
+                gemm(g, a, "tn", **kw2)                                   # layer 0: dW2 last
+            e_w = torch.cuda.Event()
+            e_w.record(side)
+        self.da_free[l % 2] = e_w
+        return dx if need_dx else g
 
     def _mask(self, l: int) -> torch.Tensor | None:
         if self.masks is None:
@@ -640,6 +689,8 @@ class FFNTrainer:
                     out = self.dxs[l % 2]
                     comm.reduce_scatter_into(out, dxp, tpg, async_op=True).wait()
                     g = out
+            elif self.wg_stream is not None:
+                g = self._layer_bwd_concurrent(l, g, w1, w2, a, h, gw1, gw2, need_dx)
             else:
                 if not keep:
                     recompute_fwd1(self.xs[l], w1, act, gated, a, h, mask=self._mask(l))
@@ -654,6 +705,9 @@ class FFNTrainer:
                     if at is not None and at > l:
                         self._zero_finish(b)
 
+        if self.wg_stream is not None:
+            # the next forward reads the updated weights (and reuses every activation buffer)
+            torch.cuda.current_stream(self.device).wait_stream(self.wg_stream)
         self._unmark(mark)
         # ---------------- optimizer ----------------
         mark = self._mark("optimizer_tail")

@@ -66,6 +66,8 @@ class TrainConfig:
     tp_overlap: bool = True          # overlap the TP dx all-reduce with the dW1 GEMM
     relu_mask: bool = True           # ReLU: the dgrad reads a 1-bit activation mask written by the forward
                                      # GEMM instead of the bf16 activation (GPU, 8-phase kernel shapes)
+    wgrad_stream: bool = False       # single device, fused optimizer: weight-gradient GEMMs on a second
+                                     # stream, concurrent with the dgrad chain (CUs shared; epilogues overlap)
     gemm_tiles_per_block: int = 0    # persistent 8-phase GEMM blocks (process-wide): tiles per block; 0 = auto
                                      # (2 for plain FFN stacks, 1 for gated stacks, where it measured slower)
     fused_optimizer: bool = True     # fuse SGD/Adam into the wgrad GEMM epilogue when no grad collective
