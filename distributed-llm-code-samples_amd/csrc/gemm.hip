@@ -394,6 +394,35 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
       for (int e = 0; e < 4; ++e) a[e] = actf<ACT>(p.act, g[e]) * u[e];
       Vec4<OutT>::store(Cp, (long)DLLM_M(rg) * p.ldc + (nb >> 5) * 16 + (nb & 15), a);
     }
+  } else if constexpr (EPI == EPI_DGLU && BF) {
+    // acc = da over the de-interleaved F axis; aux / C interleaved [g|u] 16-column blocks.  A 32-column
+    // interleaved strip [g (16) | u (16)] has exactly the paired-access shape (nt = 0 columns -> g, nt = 1
+    // columns -> u), so each row group is 2 paired 16-B loads + 2 paired 16-B stores per lane (16 rows x
+    // 64 B per instruction) instead of 4 + 4 scattered 8-B accesses.
+#pragma unroll
+    for (int b0 = 0; b0 < 16; b0 += RB) {
+      uint4 P[RB][2];
+#pragma unroll
+      for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+          P[r][nt] = *(const uint4*)((const uint16_t*)p.aux + (long)DLLM_M(b0 + r) * p.ldaux + 2 * DLLM_NB(b0 + r) +
+                                     32 * nt + pc);
+#pragma unroll
+      for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          f32x4_t g, u, dg, du;
+          unpair_bf16(P[r][nt], g, u);
+          const f32x4_t da = DLLM_ACC(b0 + r, nt);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            du[e] = da[e] * actf<ACT>(p.act, g[e]);
+            dg[e] = da[e] * u[e] * actg<ACT>(p.act, g[e]);
+          }
+          st_pair_bf16(Cp, (long)DLLM_M(b0 + r) * p.ldc + 2 * DLLM_NB(b0 + r) + 32 * nt + pc, dg, du);
+        }
+    }
   } else if constexpr (EPI == EPI_DGLU) {
     // acc = da over the de-interleaved F axis; aux / C interleaved [g|u] 16-column blocks
     using RD = typename R::type;
