@@ -115,3 +115,29 @@ def test_flops_accounting():
     unit = 2 * 8192 * 4096 * 16384
     assert flops_per_step(cfg, recompute="full", skip_dx0=False) == 8 * 7 * unit  # reference: 7 GEMMs / layer
     assert flops_per_step(cfg) == 8 * 6 * unit - unit
+
+
+def test_gemm_scheduling_knobs_cpu():
+    """Process-wide GEMM knobs round-trip without a GPU (the native library loads on CPU); ReLU-mask sizing."""
+    from dllm.ops.gemm import relu_mask_bytes, relu_mask_supported, set_tiles_per_block
+
+    old = set_tiles_per_block(4)
+    assert set_tiles_per_block(0) == 4          # <= 1 -> one block per tile
+    assert set_tiles_per_block(old) == 1
+    assert relu_mask_bytes(8192, 16384) == 32 * 64 * 8192
+    assert relu_mask_supported(8192, 16384, 4096)
+    assert not relu_mask_supported(8192, 16384, 4096 + 64)    # K % 128: 2-stage kernel, no tile-native mask
+    assert not relu_mask_supported(8192, 16384 + 128, 4096)   # N % 256
+    assert not relu_mask_supported(512, 512, 2048)            # small grid -> split-K
+    assert not relu_mask_supported(8192, 16384, 4096, torch.float32)
+
+
+def test_engine_cpu_has_no_device_side_buffers():
+    from dllm.parallel.engine import FFNTrainer
+    from dllm.parallel.mesh import Mesh
+    from dllm.utils.config import ModelConfig, TrainConfig
+
+    cfg = TrainConfig(model=ModelConfig(256, 1024, 2, "relu", False), batch_size=1, seq_len=256, dtype="bf16",
+                      wgrad_stream=True)
+    eng = FFNTrainer(cfg, Mesh(), torch.device("cpu"))
+    assert eng.masks is None and eng.wg_stream is None
