@@ -109,7 +109,7 @@ def build_tools(verbose: bool = False, force: bool = False) -> list[str]:
     return out
 
 
-def build(verbose: bool = False, force: bool = False, jobs: int = 4) -> str:
+def build(verbose: bool = False, force: bool = False, jobs: int = 0) -> str:
     """Compile all native sources for gfx950 and link ``_dllm_native.so``; returns the library path."""
     os.makedirs(BUILD, exist_ok=True)
     if force:
@@ -117,6 +117,7 @@ def build(verbose: bool = False, force: bool = False, jobs: int = 4) -> str:
             os.remove(os.path.join(BUILD, f))
     build_tools(verbose, force)
     srcs = sources()
+    jobs = jobs or min(8, os.cpu_count() or 4, len(srcs))  # the GEMM library is split per layout for this
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         objs = list(ex.map(lambda s: _compile(s, verbose), srcs))
     newest = max(os.path.getmtime(o) for o in objs)
