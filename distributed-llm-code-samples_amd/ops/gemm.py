@@ -19,7 +19,7 @@ followed by an epilogue:
   ``C += -lr·alpha·acc`` (reference ``param.add_(-LR*grad)``), ``aux_out`` = its bf16 working copy
 * ``"adam"``:  same with fused AdamW; ``opt_m``/``opt_v`` share ``C``'s layout
 
-CUDA (HIP) tensors run the hand-written gfx950 kernels of ``csrc/gemm.hip``; CPU tensors run the torch
+CUDA (HIP) tensors run the hand-written gfx950 kernels of ``csrc/gemm_kernels.h``; CPU tensors run the torch
 reference below (used by the CPU/gloo tests and as the numerics oracle).  There is no silent fallback:
 a GPU tensor with the native library missing raises.
 """
