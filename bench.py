@@ -194,6 +194,8 @@ def main() -> int:
         eng.zero_sync_state()  # quiesce in-flight weight all-gathers before teardown
     par = {"ddp": f"dp{n}", "zero": f"dp{n}-zero2", "fsdp": f"fsdp{n}", "tp": f"tp{n}",
            "hybrid": f"fsdp{dp}xtp{tp}"}[a.method]
+    if world == 1 and not a.force_comm and a.method in ("ddp", "zero", "fsdp"):
+        par = "dp1"  # one device: no gradient collective, the optimizer is fused into the wgrad GEMMs
     rec = {
         "metric": METRIC, "value": round(value, 1), "unit": "tokens/s", "n_gpus": 0 if cpu else n, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
