@@ -254,8 +254,11 @@ def _worker(method: int, local_rank: int, layers_params, seeds, batch_size: int,
     seeds = torch.as_tensor(seeds, dtype=torch.int64)
     mine = stripe_seeds(seeds, dp, mesh.dp_rank) if dp > 1 else seeds
     data = make_data("cpu_compat", cfg.tokens, D, cfg.torch_dtype, dev)
-    for s in mine.tolist():
-        x, dy = data.fill(int(s))
+    order = mine.tolist()
+    for s in order[:data.depth]:
+        data.prefetch(int(s))
+    for i, s in enumerate(order):
+        x, dy = data.fill(int(s), next_seed=order[i + data.depth] if i + data.depth < len(order) else None)
         eng.train_step(x, dy)
     res = eng.local_params()  # full over dp (FSDP gathers), this rank's TP shard
     r = dist.get_rank()

@@ -96,8 +96,10 @@ def run_rank(rank: int, world: int, cfg_dict: dict, method: int, backend: str, p
     stop_after = int(opts.get("stop_after") or len(my_seeds))
     done = start_step
     seed_list = my_seeds.tolist()
-    if start_step < len(seed_list):
-        data.prefetch(int(seed_list[start_step]))
+    depth = max(1, getattr(data, "depth", 1))  # host threads drawing upcoming batches (cpu_compat data)
+    limit = min(len(seed_list), stop_after)
+    for k in range(start_step, min(start_step + depth, limit)):
+        data.prefetch(int(seed_list[k]))
     try:
         with maybe_profile(opts.get("profile", ""), rank):
             for i, s in enumerate(seed_list):
@@ -107,7 +109,7 @@ def run_rank(rank: int, world: int, cfg_dict: dict, method: int, backend: str, p
                     break
                 _maybe_inject_fault(rank, i)
                 timer.start()
-                nxt = seed_list[i + 1] if i + 1 < min(len(seed_list), stop_after) else None
+                nxt = seed_list[i + depth] if i + depth < limit else None
                 x, dy = data.fill(int(s), next_seed=nxt)
                 eng.train_step(x, dy)
                 timer.stop()

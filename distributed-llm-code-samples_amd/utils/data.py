@@ -29,7 +29,9 @@ class DeviceMockData:
         self.x = torch.empty((tokens, model_size), dtype=dtype, device=device)
         self.dy = torch.empty((tokens, model_size), dtype=dtype, device=device)
 
-    def prefetch(self, seed: int) -> None:  # device generation needs no prefetch
+    depth = 0  # device generation needs no prefetch
+
+    def prefetch(self, seed: int) -> None:
         return None
 
     def fill(self, seed: int, next_seed: int | None = None) -> tuple[torch.Tensor, torch.Tensor]:
@@ -41,13 +43,15 @@ class DeviceMockData:
 class CpuCompatData:
     """Reference stream (CPU ``Generator``), copied into preallocated device buffers.
 
-    The reference draws each batch on the host inside the timed step (~0.4 s at T=8192, D=4096).  Here
-    a background thread draws the NEXT seed's batch into pinned host memory while the GPU trains on the
-    current one, and the copy to the device is an async H2D on the current stream.  Values are identical
-    to the reference's ``mock_data`` (same generator, same draw order)."""
+    The reference draws each batch on the host inside the timed step (~0.4 s at T=8192, D=4096, one core).
+    Every step reseeds its own generator (train_ffns.py:148), so steps are independent streams: a pool of
+    ``depth`` host threads draws the next ``depth`` seeds' batches concurrently into pinned memory while the
+    GPU trains on the current one (torch's CPU RNG releases the GIL), and the copy to the device is an async
+    H2D on the current stream.  Values are identical to the reference's ``mock_data`` (same generator, same
+    draw order per seed).  ``depth`` defaults to the host cores available to this rank (at most 8)."""
 
     def __init__(self, tokens: int, model_size: int, dtype: torch.dtype, device: torch.device,
-                 prefetch: bool = True):
+                 prefetch: bool = True, depth: int = 0):
         self.x = torch.empty((tokens, model_size), dtype=dtype, device=device)
         self.dy = torch.empty((tokens, model_size), dtype=dtype, device=device)
         self.tokens, self.model_size = tokens, model_size
@@ -55,10 +59,16 @@ class CpuCompatData:
         self.pin = self.device.type == "cuda"
         self._pool = None
         self._pending = {}
+        if not depth:
+            import os
+
+            ranks = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
+            depth = max(1, min(8, (os.cpu_count() or 2) // ranks - 1))
+        self.depth = depth if prefetch else 0
         if prefetch:
             import concurrent.futures as cf
 
-            self._pool = cf.ThreadPoolExecutor(max_workers=1)
+            self._pool = cf.ThreadPoolExecutor(max_workers=self.depth)
         self._host = None
 
     def _draw(self, seed: int):
