@@ -39,6 +39,7 @@ _SIGS = {
     "dllm_abi_version": (c_int, []),
     "dllm_gemm_set_variant": (c_int, [c_int]),
     "dllm_gemm_set_tiles_per_block": (c_int, [c_int]),
+    "dllm_gemm_set_min_blocks_per_cu": (c_int, [c_int]),
     "dllm_gemm_ablation": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
 }
 _OPTIONAL_SIGS: dict = {}

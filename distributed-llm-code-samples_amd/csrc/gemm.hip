@@ -93,6 +93,13 @@ int dllm_gemm_set_variant(int v) {
   return old;
 }
 
+// minimum blocks per CU of a persistent 8-phase grid (>= 1); returns the previous value
+int dllm_gemm_set_min_blocks_per_cu(int n) {
+  const int old = g_min_bpc;
+  g_min_bpc = n < 1 ? 1 : n;
+  return old;
+}
+
 // tiles per persistent 8-phase block (<= 1: one block per tile); returns the previous value
 int dllm_gemm_set_tiles_per_block(int t) {
   const int old = g_tpb;

@@ -1396,6 +1396,11 @@ inline int g_bf16_variant = 0;
 // tiles / CUs; at the default of 2 a block delayed by a concurrent kernel (an overlapped RCCL collective)
 // holds back at most two tiles.
 inline int g_tpb = 2;
+// Minimum blocks per CU of a persistent grid.  1 on a single device; 2 when collectives run concurrently
+// (set by the engine): an RCCL kernel holding a CU then delays one of >= 2 blocks per CU, whose tiles the
+// other CUs' later blocks absorb, instead of the only block of that CU (which would add a whole block's
+// time to the GEMM).
+inline int g_min_bpc = 1;
 constexpr int MAX_DEV = 64;
 inline int g_num_cu[MAX_DEV] = {};
 
@@ -1416,7 +1421,7 @@ static int grid_8ph(GemmArgs& a, int nb) {
   a.tpb = 1;
   const int ncu = num_cu();
   if (g_tpb <= 1 || ncu <= 0) return nb;
-  const int t = std::min(g_tpb, nb / ncu);
+  const int t = std::min(g_tpb, nb / (ncu * std::max(1, g_min_bpc)));
   if (t <= 1) return nb;
   const int g = ((nb + t - 1) / t + 7) / 8 * 8;
   if (g >= nb) return nb;

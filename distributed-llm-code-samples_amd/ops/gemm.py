@@ -277,6 +277,13 @@ def set_tiles_per_block(n: int) -> int:
     return int(_native.lib().dllm_gemm_set_tiles_per_block(int(n)))
 
 
+def set_min_blocks_per_cu(n: int) -> int:
+    """Minimum blocks per CU of a persistent GEMM grid (process-wide; default 1).  The engine sets 2 when
+    collectives run concurrently with the GEMMs, so a CU held by an RCCL kernel delays one of several blocks
+    per CU rather than the only one.  Returns the previous setting."""
+    return int(_native.lib().dllm_gemm_set_min_blocks_per_cu(int(n)))
+
+
 def gemm_path(a_dtype: torch.dtype, out_dtype: torch.dtype, M: int, N: int, K: int,
               lda: int, ldb: int, ldc: int) -> str:
     """Which native kernel family a call would use: 'mfma_bf16', 'mfma_f32' or 'generic'."""

@@ -126,9 +126,11 @@ class FFNTrainer:
         self.step_count = 0
         dev = self.device
         if dev.type == "cuda":
-            from ..ops.gemm import set_tiles_per_block
+            from ..ops.gemm import set_min_blocks_per_cu, set_tiles_per_block
 
             set_tiles_per_block(cfg.gemm_tiles_per_block or (1 if m.gated else 2))
+            # collectives overlapping the GEMMs (any multi-rank mesh, or forced size-1 communicators)
+            set_min_blocks_per_cu(2 if (mesh.world > 1 or cfg.force_comm) else 1)
         if cfg.debug_sync:
             comm.set_serialize(True)
         # custom xGMI all-reduce for the TP activation exchange (opt-in; gradients stay on RCCL)

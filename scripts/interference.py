@@ -31,7 +31,13 @@ def main():
     ap.add_argument("--cus", default="0,8,16,32,64")
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--json", default="")
+    ap.add_argument("--tpb", type=int, default=2, help="tiles per persistent GEMM block (1 = off)")
+    ap.add_argument("--min_bpc", type=int, default=1, help="minimum persistent blocks per CU")
     a = ap.parse_args()
+    from dllm.ops.gemm import set_min_blocks_per_cu, set_tiles_per_block
+
+    set_tiles_per_block(a.tpb)
+    set_min_blocks_per_cu(a.min_bpc)
     T, D, F = a.T, a.D, a.F
     bf, dev = torch.bfloat16, "cuda"
     x = torch.randn(T, D, device=dev, dtype=bf)
@@ -46,7 +52,7 @@ def main():
         "fwd1 NT act (2048 tiles)": lambda: gemm(x, w1, "nt", out=out_tf, epi="act", act="relu"),
         "fwd2 NT (512 tiles)": lambda: gemm(h, w2, "nt", out=out_td),
         "wgrad TN bf16 (1024 tiles)": lambda: gemm(dy, h, "tn", out=g),
-        "torch fwd2": lambda: torch.matmul(h, w2.t(), out=out_td),
+        "dx-shape NN (512 tiles)": lambda: gemm(h, w1, "nn", out=out_td),
     }
     lib = _native.lib()
     side = torch.cuda.Stream()
