@@ -11,4 +11,6 @@ b c4_tp_F14336_L1_full --steps 20 --warmup 5 --method tp --ffn_dim 14336 --layer
 b c4_tp8_rank_shard_F1792 --steps 20 --warmup 5 --method tp --ffn_dim 1792 --layers 1
 b c5_llama3_8b_ffn_L32_swiglu --steps 4 --warmup 2 --method hybrid --tp 1 --gated --act silu --ffn_dim 14336 --layers 32
 b c5_llama3_8b_ffn_L32_swiglu_adam --steps 4 --warmup 2 --method hybrid --tp 1 --gated --act silu --ffn_dim 14336 --layers 32 --optimizer adam
+# the reference's memory example (train_ffns.py:8-10): D=8192 L=8 "does not fit with DDP" on 4x24 GB -- one MI355X holds it
+b c6_ref_memory_example_D8192_L8 --steps 4 --warmup 2 --method ddp --model_size 8192 --layers 8
 cat $OUT
