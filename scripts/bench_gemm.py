@@ -77,8 +77,6 @@ def main():
     if a.cases:
         cases = {k: v for k, v in cases.items() if any(c in k for c in a.cases.split(","))}
     for name, (mine, ref) in cases.items():
-        if a.no_torch:
-            ref = lambda: None  # noqa: E731
         times = {v: [] for v in variants}
         tr = []
         for _ in range(a.rounds):  # interleaved rounds in one process (guide §5.4 rule 24)
@@ -90,10 +88,13 @@ def main():
                     set_bf16_variant(v)
                     set_tiles_per_block(1)
                 times[v].append(timeit(mine, a.iters))
-            tr.append(timeit(ref, a.iters))
-        r = statistics.median(tr)
-        row = {"torch_ms": r, "torch_tflops": flops / r / 1e9}
-        msg = f"{name:26s} torch {flops / r / 1e9:7.1f} TF |"
+            if not a.no_torch:
+                tr.append(timeit(ref, a.iters))
+        row, msg = {}, f"{name:26s}"
+        if tr:  # --no_torch: hipBLASLt not timed, no torch fields
+            r = statistics.median(tr)
+            row = {"torch_ms": r, "torch_tflops": flops / r / 1e9}
+            msg += f" torch {flops / r / 1e9:7.1f} TF |"
         for v in variants:
             m = statistics.median(times[v])
             row[v + "_ms"], row[v + "_tflops"] = m, flops / m / 1e9

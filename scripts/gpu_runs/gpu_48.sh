@@ -1,5 +1,5 @@
 #!/bin/bash
-# Full validation of the current tree: GPU test suite, smoke(), default bench, CPU-compat CLI step.
+# Full validation of the current tree: GPU test suite, smoke(), default bench.
 source scripts/gpu_steps.sh
 step gputests 1000 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
