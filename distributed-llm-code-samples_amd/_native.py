@@ -54,8 +54,8 @@ def register_optional(name: str, restype, argtypes) -> None:
 
 
 def _load() -> ctypes.CDLL:
-    path = _build.LIB_PATH
-    if not os.path.exists(path) or os.environ.get("DLLM_REBUILD") == "1":
+    path = os.environ.get("DLLM_NATIVE_LIB") or _build.LIB_PATH  # alternate build (A/B experiments)
+    if path == _build.LIB_PATH and (not os.path.exists(path) or os.environ.get("DLLM_REBUILD") == "1"):
         _build.build()
     lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
     for name, (res, args) in {**_SIGS, **_OPTIONAL_SIGS}.items():
