@@ -10,16 +10,34 @@ reference optimizer, train_ffns.py:172), random-init weights and synthetic devic
 
 Each timed step is the full training step: device mock-data generation, forward, backward (all weight
 and input gradients except the unused layer-0 input grad), gradient communication and the optimizer
-update.  Default parallelism for N>1 is data parallel with ZeRO-2 sharding (bf16 gradient reduce-scatter,
-fp32 master weights sharded 1/N, bf16 weight all-gather); with N=1 there is no gradient collective and
-the SGD update is fused into the weight-gradient GEMM epilogues.  K steps are bracketed by cuda synchronize + barrier on both sides; the max over ranks is
-reported; rank 0 prints ONE JSON line.  Weak scaling: every rank processes 8192 tokens per step under
-DDP/FSDP (global batch = 8·N sequences); ``--method tp`` shards each layer over the GPUs instead
-(tokens per step fixed: strong scaling).
+update.  K steps are bracketed by cuda synchronize + barrier on both sides; the max over ranks is
+reported; rank 0 prints ONE JSON line.
+
+Headline (``value``): ``--method`` (default ``zero``) on the 8-layer stack.  ``zero`` is data parallel
+with DDP semantics (identical updates to DDP: summed gradients, every rank's replica updated) carried
+as ZeRO-2: bucketed bf16 gradient reduce-scatter overlapped with the backward, fp32 master / optimizer
+state sharded 1/N, bf16 weight all-gather overlapped with the next forward.  With N=1 there is no
+gradient collective and the SGD update is fused into the weight-gradient GEMM epilogues (``dp1``).
+
+``methods``: the reference's methods timed side by side like its ``--method 0`` (train_ffns.py:373-384),
+each on its own engine at the same N, with steady-state tokens/s, ms/step, peak HBM and (when the method
+communicates) per-role collective time and the fraction of it hidden under the GEMMs (comm observer,
+utils/observe.py, measured on extra steps after the timed ones):
+
+* ``ddp``   bucketed gradient all-reduce + full optimizer on every rank (train_ffns.py:156-193);
+* ``zero``  as the headline;
+* ``fsdp``  ZeRO-3 row shards, prefetched all-gathers, async reduce-scatter (train_ffns.py:197-287);
+* ``tp``    the MP config of BASELINE.json: hidden 4096, FFN 14336, one layer, column/row split over the
+            N GPUs (train_ffns.py:290-338; every rank sees every token: strong scaling).
+
+At N=1 the ddp/zero/fsdp/tp entries run their collective code paths over size-1 communicators
+(``force_comm``), so each method's own overhead is visible even on one GPU.  Weak scaling for the DP
+methods: every rank processes 8192 tokens per step (global batch = 8·N sequences).
 """
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -36,20 +54,27 @@ from dllm.utils.data import DeviceMockData
 from dllm.utils.metrics import PEAK_TFLOPS, flops_per_step
 
 METRIC = "FFN tokens/sec (whole node) at hidden=4096 for DDP/FSDP/MP, 1/2/4/8 MI355X"
+MP_FFN = 14336  # BASELINE.json config 4: FFN (hidden=4096, ffn=14336) MP column/row split
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=0)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--method", choices=["ddp", "zero", "fsdp", "tp", "hybrid"], default="zero",
-                   help="zero = data parallel with ZeRO-2 (bucketed reduce-scatter overlapped with the backward, "
-                        "1/N sharded optimizer, async all-gather of the bf16 weights overlapped with the next "
-                        "forward); ddp = bucketed all-reduce + full optimizer per rank")
+                   help="headline method (see module docstring); zero = DDP semantics as ZeRO-2")
+    p.add_argument("--methods", default="ddp,zero,fsdp,tp",
+                   help="comma list of methods also timed side by side ('' or 'none' = headline only)")
+    p.add_argument("--method_steps", type=int, default=0,
+                   help="timed steps per side-by-side method (0 = min(steps, 10))")
+    p.add_argument("--observe_steps", type=int, default=2,
+                   help="extra steps per communicating method under the comm observer (0 = off)")
     p.add_argument("--tp", type=int, default=0, help="TP degree for --method hybrid")
     p.add_argument("--model_size", type=int, default=4096)
     p.add_argument("--ffn_dim", type=int, default=0)
+    p.add_argument("--mp_ffn_dim", type=int, default=MP_FFN, help="FFN width of the tp (MP) method entry")
+    p.add_argument("--mp_layers", type=int, default=1, help="layers of the tp (MP) method entry")
     p.add_argument("--layers", type=int, default=8)
     p.add_argument("--batch_size", type=int, default=8)
     p.add_argument("--seq_len", type=int, default=1024)
@@ -84,8 +109,6 @@ def parse():
     p.add_argument("--gemm_variant", default="auto",
                    choices=["auto", "2stage", "8phase", "8phase_stagger", "4phase_stagger"],
                    help="bf16 GEMM main-loop schedule (auto = 8-phase staggered when K % 128 == 0)")
-    p.add_argument("--lib_plain_nt", action="store_true",
-                   help="run the plain forward GEMM y = a·W2ᵀ (no epilogue) on hipBLASLt; all fused GEMMs stay native")
     p.add_argument("--tpb", type=int, default=0,
                    help="tiles per persistent 8-phase GEMM block (0 = auto: 2, or 1 for gated stacks; 1 = off)")
     p.add_argument("--wgrad_stream", action="store_true",
@@ -93,70 +116,92 @@ def parse():
     p.add_argument("--no_relu_mask", action="store_true",
                    help="ReLU dgrad reads the bf16 activation instead of the forward's 1-bit mask")
     p.add_argument("--force_comm", action="store_true",
-                   help="exercise the RCCL DDP/FSDP path at N=1 (size-1 communicators, unfused optimizer)")
-    return p.parse_args()
+                   help="exercise the RCCL DDP/FSDP path of the headline at N=1 (size-1 communicators)")
+    return p.parse_args(argv)
 
 
-def main() -> int:
-    a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    n = a.gpus or world
-    if n != world:
-        raise SystemExit(f"--gpus {n} but WORLD_SIZE={world}: launch N>1 with torchrun")
-    cpu = a.backend == "gloo"
-    if world > 1 or a.force_comm:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29533")
-        init_distributed(a.backend)
-    elif not cpu:
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
-    dev = torch.device("cpu") if cpu else torch.device("cuda", torch.cuda.current_device())
+def mesh_of(method: str, n: int, tp_arg: int) -> tuple[str, int, int]:
+    """(dp_mode, dp, tp) of a method on n ranks."""
+    if method in ("ddp", "zero", "fsdp"):
+        return method, n, 1
+    if method == "tp":
+        return "none", 1, n
+    tp = tp_arg or min(n, 2)
+    return "fsdp", n // tp, tp
+
+
+def parallelism(method, n, dp, tp, world, force_comm) -> str:
+    if world == 1 and not force_comm and method in ("ddp", "zero", "fsdp"):
+        return "dp1"  # one device: no gradient collective, the optimizer is fused into the wgrad GEMMs
+    return {"ddp": f"dp{n}", "zero": f"dp{n}-zero2", "fsdp": f"fsdp{n}", "tp": f"tp{n}",
+            "hybrid": f"fsdp{dp}xtp{tp}"}[method] + ("-forcecomm" if world == 1 and force_comm else "")
+
+
+def model_name(m: ModelConfig) -> str:
+    return f"ffn-stack L{m.layers} D{m.D} F{m.F} {'swiglu-' if m.gated else ''}{m.act}"
+
+
+def state_gib(eng) -> dict:
+    """Per-rank persistent training state (GiB): fp32 master (+ optimizer moments), compute copy, grads."""
+    g = lambda t: round(t.numel() * t.element_size() / 2**30, 3)  # noqa: E731
+    out = {"master_fp32": g(eng.master), "compute_copy": 0.0 if eng.shared_copy else g(eng.copy),
+           "grads": g(eng.grads)}
+    if getattr(eng, "adam_m", None) is not None:
+        out["adam_mv"] = round(2 * g(eng.adam_m), 3)
+    return out
+
+
+def destroy_mesh(mesh: Mesh) -> None:
+    """Tear down this method's communicators (native ones and torch role process groups) so the next
+    method's mesh does not hold stale RCCL resources."""
+    import torch.distributed as dist
+
+    torch_groups = [g for g in mesh.groups.values()
+                    if isinstance(g, dist.ProcessGroup) and g is not dist.GroupMember.WORLD]
+    mesh.destroy()
+    if dist.is_initialized():
+        dist.barrier()
+        seen = set()
+        for g in torch_groups:
+            if id(g) not in seen:
+                seen.add(id(g))
+                dist.destroy_process_group(g)
+
+
+def run_method(a, method: str, n: int, world: int, dev: torch.device, steps: int, warmup: int,
+               force_comm: bool, model: ModelConfig, observe_steps: int = 0, headline: bool = False) -> dict:
+    """Build the engine for ``method`` on ``n`` ranks, run ``warmup`` untimed + ``steps`` timed steps (+ the
+    observed steps), return the method's record.  Collective over all ranks."""
+    cpu = dev.type == "cpu"
     sync = (lambda: None) if cpu else torch.cuda.synchronize
-
-    if a.method == "ddp":
-        dp_mode, dp, tp = "ddp", n, 1
-    elif a.method == "zero":
-        dp_mode, dp, tp = "zero", n, 1
-    elif a.method == "fsdp":
-        dp_mode, dp, tp = "fsdp", n, 1
-    elif a.method == "tp":
-        dp_mode, dp, tp = "none", 1, n
-    else:
-        tp = a.tp or min(n, 2)
-        dp_mode, dp = "fsdp", n // tp
-    if a.gemm_variant != "auto" and not cpu:
-        from dllm.ops.gemm import set_bf16_variant
-
-        set_bf16_variant(a.gemm_variant)
-    if a.lib_plain_nt:
-        from dllm.ops.gemm import set_library_plain_nt
-
-        set_library_plain_nt(True)
-    m = ModelConfig(model_size=a.model_size, ffn_dim=a.ffn_dim, layers=a.layers, act=a.act, gated=a.gated)
-    cfg = TrainConfig(model=m, batch_size=a.batch_size, seq_len=a.seq_len, num_steps=a.steps, dtype=a.dtype,
+    dp_mode, dp, tp = mesh_of(method, n, a.tp)
+    cfg = TrainConfig(model=model, batch_size=a.batch_size, seq_len=a.seq_len, num_steps=steps, dtype=a.dtype,
                       grad_dtype=a.grad_dtype, optimizer=a.optimizer, dp_mode=dp_mode, dp=dp, tp=tp,
                       bucket_mb=a.bucket_mb, recompute=a.recompute, sequence_parallel=a.sequence_parallel,
-                      data="device", force_comm=a.force_comm, comm_backend=a.comm, side_optimizer=a.side_opt, tp_allreduce=a.tp_allreduce,
+                      data="device", force_comm=force_comm, comm_backend=a.comm,
+                      side_optimizer=a.side_opt if headline else 0, tp_allreduce=a.tp_allreduce,
                       relu_mask=not a.no_relu_mask, gemm_tiles_per_block=a.tpb,
-                      wgrad_stream=a.wgrad_stream)
-    mesh = Mesh.build(dp, tp, force=a.force_comm, comm_backend="torch" if cpu else a.comm,
+                      wgrad_stream=a.wgrad_stream and headline)
+    mesh = Mesh.build(dp, tp, force=force_comm, comm_backend="torch" if cpu else a.comm,
                       device=None if cpu else dev)
+    if not cpu:
+        torch.cuda.reset_peak_memory_stats(dev)
     eng = FFNTrainer(cfg, mesh, dev)
     from dllm.models.ffn import init_ffn_params_device
 
-    init_scale = ("fan_in" if m.gated else 2e-2) if a.init_scale == "auto" else (
+    init_scale = ("fan_in" if model.gated else 2e-2) if a.init_scale == "auto" else (
         a.init_scale if a.init_scale == "fan_in" else float(a.init_scale))
-    eng.load_full_params(init_ffn_params_device(m.D, m.F, m.layers, a.seed, dev, m.gated, scale=init_scale))
+    eng.load_full_params(init_ffn_params_device(model.D, model.F, model.layers, a.seed, dev, model.gated,
+                                                scale=init_scale))
     sync()
-    data = DeviceMockData(cfg.tokens, m.D, cfg.torch_dtype, dev)
+    data = DeviceMockData(cfg.tokens, model.D, cfg.torch_dtype, dev)
     seed_base = 10_000 * (mesh.dp_rank + 1)
 
     graphed = None
-    if a.graph:
+    if a.graph and headline:
         from dllm.utils.graphs import GraphedStep
 
-        graphed = GraphedStep(eng, cfg.tokens, m.D)
+        graphed = GraphedStep(eng, cfg.tokens, model.D)
 
     def one_step(seed):
         if graphed is not None:
@@ -165,57 +210,117 @@ def main() -> int:
             x, dy = data.fill(seed)
             eng.train_step(x, dy)
 
-    for i in range(a.warmup):
+    for i in range(warmup):
         one_step(seed_base + i)
-    if a.phases and not cpu and graphed is None:
+    if a.phases and headline and not cpu and graphed is None:
         eng.enable_phase_timing(True)
     sync()
     comm.barrier(device=dev)
     t0 = time.perf_counter()
-    for i in range(a.steps):
-        one_step(seed_base + a.warmup + i)
+    for i in range(steps):
+        one_step(seed_base + warmup + i)
     sync()
     comm.barrier(device=dev)
     el = time.perf_counter() - t0
-    phases = {k: round(v / a.steps, 3) for k, v in eng.phase_summary().items()} if a.phases else None
+    eng.check_health()
+    phases = {k: round(v / steps, 3) for k, v in eng.phase_summary().items()} if (a.phases and headline) else None
     if world > 1:
         import torch.distributed as dist
 
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    ms = el / a.steps * 1e3
-    tokens_global = cfg.tokens * dp
-    value = tokens_global * a.steps / el
-    tflops = flops_per_step(cfg, tp=tp, recompute=cfg.recompute) / (ms / 1e3) / 1e12
-    finite = bool(torch.isfinite(eng.master[:1024]).all().item())
-    peak_gib = 0.0 if cpu else torch.cuda.max_memory_allocated(dev) / 2**30
-    if eng.zero:
-        eng.zero_sync_state()  # quiesce in-flight weight all-gathers before teardown
-    par = {"ddp": f"dp{n}", "zero": f"dp{n}-zero2", "fsdp": f"fsdp{n}", "tp": f"tp{n}",
-           "hybrid": f"fsdp{dp}xtp{tp}"}[a.method]
-    if world == 1 and not a.force_comm and a.method in ("ddp", "zero", "fsdp"):
-        par = "dp1"  # one device: no gradient collective, the optimizer is fused into the wgrad GEMMs
-    rec = {
-        "metric": METRIC, "value": round(value, 1), "unit": "tokens/s", "n_gpus": 0 if cpu else n, "steps": a.steps,
-        "warmup": a.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
-        "scaling": "strong" if a.method == "tp" else "weak", "vs_baseline": None, "dtype": a.dtype,
-        "data": "synthetic (device Philox N(0,1) x, 0.1*N(0,1) dloss/dx; random-init weights)",
-        "config": {"model": f"ffn-stack L{m.layers} D{m.D} F{m.F} {'swiglu-' if m.gated else ''}{m.act}",
-                   "global_batch": a.batch_size * dp, "seq_len": a.seq_len, "parallelism": par,
-                   "optimizer": a.optimizer, "grad_dtype": a.grad_dtype, "master_weights": "fp32",
-                   "init_scale": init_scale},
-        "tflops_per_gpu": round(tflops, 1), "mfu_dense": round(tflops / PEAK_TFLOPS[a.dtype], 4),
-        "peak_hbm_gib": round(peak_gib, 2), "finite": finite, "comm": a.comm, "hip_graph": bool(a.graph),
-        "plain_nt_gemm": "hipblaslt" if a.lib_plain_nt else "native", "gemm_variant": a.gemm_variant,
-        "gemm_tiles_per_block": a.tpb or ("auto: 1" if m.gated else "auto: 2"), "relu_mask": eng.masks is not None,
-        "wgrad_stream": eng.wg_stream is not None,
-        "tp_allreduce": a.tp_allreduce,
-    }
+    ms = el / steps * 1e3
+    rec = {"value": round(cfg.tokens * dp * steps / el, 1), "ms_per_step": round(ms, 3),
+           "tflops_per_gpu": round(flops_per_step(cfg, tp=tp, recompute=cfg.recompute) / (ms / 1e3) / 1e12, 1),
+           "peak_hbm_gib": 0.0 if cpu else round(torch.cuda.max_memory_allocated(dev) / 2**30, 2),
+           "finite": bool(torch.isfinite(eng.master[:1024]).all().item()),
+           "global_batch": a.batch_size * dp, "parallelism": parallelism(method, n, dp, tp, world, force_comm),
+           "model": model_name(model), "steps": steps, "warmup": warmup, "state_gib": state_gib(eng)}
     if phases:
         rec["phase_ms_per_step"] = phases
+    communicates = bool(mesh.groups) or eng.tp_car is not None
+    if observe_steps > 0 and communicates and not cpu and graphed is None:
+        from dllm.utils.observe import CommObserver
+
+        with CommObserver(dev, dict(mesh.groups)) as obs:
+            for i in range(observe_steps):
+                one_step(seed_base + warmup + steps + i)
+        rec["comm"] = obs.summary(observe_steps)
+    if eng.zero:
+        eng.zero_sync_state()  # quiesce in-flight weight all-gathers before teardown
+    sync()
+    destroy_mesh(mesh)
+    del eng, data, graphed
+    gc.collect()
+    if not cpu:
+        torch.cuda.empty_cache()
+    return rec
+
+
+SIDE_KEYS = ("value", "ms_per_step", "tflops_per_gpu", "peak_hbm_gib", "parallelism", "model", "global_batch",
+             "steps", "finite", "state_gib", "comm")
+
+
+def main(argv=None) -> int:
+    a = parse(argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    n = a.gpus or world
+    if n != world:
+        raise SystemExit(f"--gpus {n} but WORLD_SIZE={world}: launch N>1 with torchrun")
+    cpu = a.backend == "gloo"
+    methods = [m for m in a.methods.split(",") if m and m != "none"]
+    if world > 1 or a.force_comm or methods:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        init_distributed(a.backend)
+    elif not cpu:
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    dev = torch.device("cpu") if cpu else torch.device("cuda", torch.cuda.current_device())
+    if a.gemm_variant != "auto" and not cpu:
+        from dllm.ops.gemm import set_bf16_variant
+
+        set_bf16_variant(a.gemm_variant)
+    ffn = a.ffn_dim or (a.mp_ffn_dim if a.method == "tp" else 0)
+    model = ModelConfig(model_size=a.model_size, ffn_dim=ffn, layers=a.layers, act=a.act, gated=a.gated)
+    head = run_method(a, a.method, n, world, dev, a.steps, a.warmup, a.force_comm, model,
+                      observe_steps=a.observe_steps, headline=True)
+
+    side = {}
+    for m in methods:
+        mm = model
+        if m == "tp":
+            mm = ModelConfig(model_size=a.model_size, ffn_dim=a.mp_ffn_dim, layers=a.mp_layers, act=a.act,
+                             gated=a.gated)
+        r = run_method(a, m, n, world, dev, a.method_steps or min(a.steps, 10), min(a.warmup, 3),
+                       force_comm=(world == 1), model=mm, observe_steps=a.observe_steps)
+        side[m] = {k: r[k] for k in SIDE_KEYS if k in r}
+
+    rec = {
+        "metric": METRIC, "value": head["value"], "unit": "tokens/s", "n_gpus": 0 if cpu else n, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": head["ms_per_step"], "higher_is_better": True,
+        "scaling": "strong" if a.method == "tp" else "weak", "vs_baseline": None, "dtype": a.dtype,
+        "data": "synthetic (device Philox N(0,1) x, 0.1*N(0,1) dloss/dx; random-init weights)",
+        "config": {"model": head["model"], "global_batch": head["global_batch"], "seq_len": a.seq_len,
+                   "parallelism": head["parallelism"], "optimizer": a.optimizer, "grad_dtype": a.grad_dtype,
+                   "master_weights": "fp32"},
+        "tflops_per_gpu": head["tflops_per_gpu"],
+        "mfu_dense": round(head["tflops_per_gpu"] / PEAK_TFLOPS[a.dtype], 4),
+        "peak_hbm_gib": head["peak_hbm_gib"], "state_gib": head["state_gib"], "finite": head["finite"],
+        "comm_backend": a.comm, "hip_graph": bool(a.graph), "gemm_variant": a.gemm_variant,
+        "tp_allreduce": a.tp_allreduce,
+    }
+    for k in ("comm", "phase_ms_per_step"):
+        if k in head:
+            rec[k] = head[k]
+    if side:
+        rec["methods"] = side
+        if world == 1:
+            rec["methods_note"] = ("N=1: ddp/zero/fsdp/tp run their collective code paths over size-1 "
+                                   "communicators; tp is the MP config (hidden 4096, FFN 14336, 1 layer)")
     if a.force_comm:
-        rec["note"] = "force_comm: DDP/FSDP collectives over size-1 RCCL communicators"
+        rec["note"] = "force_comm: headline collectives over size-1 RCCL communicators"
     if cpu:
         rec["note"] = f"CPU/gloo dry run with {world} ranks (plumbing only, not a measurement)"
     if rank == 0:
@@ -227,7 +332,6 @@ def main() -> int:
 
     if dist.is_initialized():
         dist.barrier()
-        mesh.destroy()
         dist.destroy_process_group()
     return 0
 

@@ -26,7 +26,7 @@ _SIGS = {
     "dllm_gemm": (c_int, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_long, c_void_p, c_long, c_void_p, c_long,
                           c_void_p, c_void_p, c_long, c_int, c_int, c_int, c_float, c_float, c_int, c_int, c_void_p,
                           c_float, c_float, c_float, c_float, c_float, c_int, c_void_p, c_void_p, c_int, c_void_p,
-                          c_void_p]),
+                          c_void_p, c_int, c_int, c_int]),
     "dllm_gemm_path": (c_int, [c_int, c_int, c_int, c_int, c_int, c_long, c_long, c_long]),
     "dllm_rng_normal": (c_int, [c_void_p, c_int, c_long, c_ull, c_ull, c_float, c_void_p]),
     "dllm_rng_normal_devseed": (c_int, [c_void_p, c_int, c_long, c_void_p, c_ull, c_float, c_void_p]),
@@ -37,10 +37,6 @@ _SIGS = {
                                c_float, c_float, c_float, c_int, c_float, c_void_p]),
     "dllm_cast": (c_int, [c_void_p, c_int, c_void_p, c_int, c_long, c_void_p]),
     "dllm_abi_version": (c_int, []),
-    "dllm_gemm_set_variant": (c_int, [c_int]),
-    "dllm_gemm_set_tiles_per_block": (c_int, [c_int]),
-    "dllm_gemm_set_min_blocks_per_cu": (c_int, [c_int]),
-    "dllm_gemm_ablation": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
 }
 _OPTIONAL_SIGS: dict = {}
 

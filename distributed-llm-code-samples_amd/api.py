@@ -232,7 +232,7 @@ def _worker(method: int, local_rank: int, layers_params, seeds, batch_size: int,
     from .parallel.engine import FFNTrainer
     from .parallel.launch import METHOD_MESH
     from .parallel.mesh import Mesh
-    from .utils.data import make_data, stripe_seeds
+    from .utils.data import make_data
 
     n = dist.get_world_size()
     on_gpu = dist.get_backend() == "nccl"
@@ -251,8 +251,9 @@ def _worker(method: int, local_rank: int, layers_params, seeds, batch_size: int,
     mesh = Mesh.build(dp, tp, device=dev if on_gpu else None)
     eng = FFNTrainer(cfg, mesh, dev)
     eng.load_full_params(full)
-    seeds = torch.as_tensor(seeds, dtype=torch.int64)
-    mine = stripe_seeds(seeds, dp, mesh.dp_rank) if dp > 1 else seeds
+    # ``seeds`` are already this rank's own: the reference's drivers hand each DDP/FSDP worker its stripe
+    # (cpus_seeds[rank], :182, :273) and every TP worker all seeds (:324)
+    mine = torch.as_tensor(seeds, dtype=torch.int64)
     data = make_data("cpu_compat", cfg.tokens, D, cfg.torch_dtype, dev)
     order = mine.tolist()
     for s in order[:data.depth]:

@@ -56,10 +56,15 @@ __device__ __forceinline__ void block_release() {
   if (threadIdx.x == 0) fence_release_sys();
 }
 
-__global__ void copy_kernel(uint4* __restrict__ dst, const uint4* __restrict__ src, long n16) {
+// err != nullptr (the copy-out): a barrier of this all-reduce timed out, so the OUT region may hold a partial
+// or stale sum -- the result is poisoned with NaN (all-ones words) instead, so a stalled peer can never turn
+// into silently wrong activations, and the host raises at its next check (CustomAllReduce.check).
+__global__ void copy_kernel(uint4* __restrict__ dst, const uint4* __restrict__ src, long n16, const int* err) {
   block_acquire();
+  const bool bad = err != nullptr && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  const uint4 nan = uint4{0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n16; i += (long)gridDim.x * blockDim.x)
-    dst[i] = src[i];
+    dst[i] = bad ? nan : src[i];
   block_release();
 }
 
@@ -69,7 +74,10 @@ __global__ void barrier_kernel(Ptrs peers, int rank, int n, long sig_off, unsign
                                int* err) {
   const int t = threadIdx.x;
   fence_release_sys();
-  if (t < n) {
+  // after a timeout the epochs of the ranks no longer line up: every later barrier fails fast (no spin)
+  // until the state is recreated, and every later result is poisoned by the copy-out
+  const bool failed = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  if (t < n && !failed) {
     unsigned* slot = (unsigned*)(peers.p[t] + sig_off + rank * 64);
     __hip_atomic_store(slot, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     unsigned* mine = (unsigned*)(peers.p[rank] + sig_off + t * 64);
@@ -214,7 +222,8 @@ int dllm_car_all_reduce(void* st, void* data, long nbytes, int dtype, double tim
   const long ticks = (long)(timeout_s * 1e8);
   const long sig_off = 2 * s->cap;
   const int cgrid = (int)std::min<long>((n16 + 255) / 256, 1024);
-  hipLaunchKernelGGL(copy_kernel, dim3(cgrid), dim3(256), 0, q, (uint4*)s->buf, (const uint4*)data, n16);
+  hipLaunchKernelGGL(copy_kernel, dim3(cgrid), dim3(256), 0, q, (uint4*)s->buf, (const uint4*)data, n16,
+                     (const int*)nullptr);
   if (s->n > 1) {
     hipLaunchKernelGGL(barrier_kernel, dim3(1), dim3(64), 0, q, s->peers, s->rank, s->n, sig_off, ++s->epoch, ticks,
                        s->err);
@@ -229,14 +238,16 @@ int dllm_car_all_reduce(void* st, void* data, long nbytes, int dtype, double tim
     }
     hipLaunchKernelGGL(barrier_kernel, dim3(1), dim3(64), 0, q, s->peers, s->rank, s->n, sig_off, ++s->epoch, ticks,
                        s->err);
-    hipLaunchKernelGGL(copy_kernel, dim3(cgrid), dim3(256), 0, q, (uint4*)data, (const uint4*)(s->buf + s->cap), n16);
+    hipLaunchKernelGGL(copy_kernel, dim3(cgrid), dim3(256), 0, q, (uint4*)data, (const uint4*)(s->buf + s->cap), n16,
+                       (const int*)s->err);
   } else {
-    hipLaunchKernelGGL(copy_kernel, dim3(cgrid), dim3(256), 0, q, (uint4*)data, (const uint4*)s->buf, n16);
+    hipLaunchKernelGGL(copy_kernel, dim3(cgrid), dim3(256), 0, q, (uint4*)data, (const uint4*)s->buf, n16,
+                       (const int*)nullptr);
   }
   return (int)hipGetLastError();
 }
 
-// 0 = ok, 1 = a barrier timed out (read after synchronising the stream)
+// 0 = ok, 1 = a barrier timed out (read after synchronising the stream); sticky until destroy
 int dllm_car_error(void* st) {
   State* s = (State*)st;
   int h = 0;

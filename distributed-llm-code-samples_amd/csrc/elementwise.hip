@@ -178,14 +178,6 @@ static inline int grid_for(long n4) {
 
 using namespace dllm;
 
-// see dllm_occupy_cus
-__global__ __launch_bounds__(64) void occupy_kernel(long ticks) {
-  __shared__ char hold[96 * 1024];
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  while ((long)(__builtin_amdgcn_s_memrealtime() - t0) < ticks) __builtin_amdgcn_s_sleep(8);
-  if (threadIdx.x == 1023) hold[ticks & 1023] = 0;  // keeps the LDS allocation
-}
-
 extern "C" {
 
 static int rng_launch(void* out, int dtype, long n, unsigned long long seed, unsigned long long offset, float scale,
@@ -253,16 +245,6 @@ int dllm_cast(const void* in, int in_dtype, void* out, int out_dtype, long n, vo
   return (int)hipGetLastError();
 }
 
-// Interference probe (performance investigation only): `nblocks` single-wave workgroups, each holding
-// 96 KiB of LDS (at most one per CU, and no 128-KiB GEMM block can share the CU), spin for `usec`
-// microseconds on the 100-MHz s_memrealtime clock -- a stand-in for RCCL channel workgroups occupying
-// CUs while a collective overlaps the GEMMs (scripts/interference.py).
-int dllm_occupy_cus(int nblocks, int usec, void* stream) {
-  if (nblocks <= 0 || usec <= 0) return -1;
-  hipLaunchKernelGGL(occupy_kernel, dim3(nblocks), dim3(64), 0, (hipStream_t)stream, (long)usec * 100);
-  return (int)hipGetLastError();
-}
-
-int dllm_abi_version() { return 2; }
+int dllm_abi_version() { return 3; }
 
 }  // extern "C"

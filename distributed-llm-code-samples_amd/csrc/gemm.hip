@@ -1,6 +1,7 @@
 // C ABI of the GEMM library (ctypes, ops/gemm.py): argument checks, kernel-family selection, dispatch to
 // the per-layout translation units.  Kernels and launch templates: gemm_kernels.h.
 #include <cmath>
+#include <cstdint>
 
 #include "gemm_kernels.h"
 
@@ -14,7 +15,7 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
               const void* B, long ldb, void* C, long ldc, const void* aux, void* aux_out, long ldaux,
               int M, int N, int K, float alpha, float beta, int group_m, int force_path, void* stream,
               float lr, float b1, float b2, float eps, float wd, int step, float* opt_m, float* opt_v,
-              int ksplit, float* workspace, void* mask) {
+              int ksplit, float* workspace, void* mask, int variant, int tpb, int min_bpc) {
   if (M <= 0 || N <= 0 || K <= 0) return -1;
   if (layout < 0 || layout > 2) return -1;
   if ((epi == EPI_GLU || epi == EPI_DGLU) && (N % 32) != 0) return -1;
@@ -28,6 +29,14 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
   a.ksplit = 1;
   a.tpb = 1;
   a.mask = nullptr;
+  a.variant = variant < 0 || variant > 4 ? 0 : variant;
+  a.tpb_req = tpb;
+  a.min_bpc = min_bpc < 1 ? 1 : min_bpc;
+  a.ws = nullptr;
+  // the LDS-DMA loads and 16-B / paired epilogue accesses of the MFMA paths need 16-B aligned bases
+  const bool aligned_ptr = ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && ((uintptr_t)C % 16 == 0) &&
+                           ((uintptr_t)aux % 16 == 0) && ((uintptr_t)aux_out % 16 == 0) &&
+                           ((uintptr_t)opt_m % 16 == 0) && ((uintptr_t)opt_v % 16 == 0);
   const bool opt_epi = (epi == EPI_SGD || epi == EPI_ADAM);
   if (opt_epi && (layout != L_TN || out_dtype != DT_F32)) return -1;
   if (epi == EPI_ADAM) {
@@ -36,7 +45,7 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
     a.bc2 = 1.f - powf(b2, (float)step);
   }
   int path = 2;
-  const bool aligned_lds = (lda % 8 == 0) && (ldb % 8 == 0) && (ldc % 4 == 0) && (ldaux % 4 == 0);
+  const bool aligned_lds = aligned_ptr && (lda % 8 == 0) && (ldb % 8 == 0) && (ldc % 4 == 0) && (ldaux % 4 == 0);
   if (in_dtype == DT_BF16 && M % BT_M == 0 && N % BT_N == 0 && K % BT_K == 0 && aligned_lds) path = 0;
   if (in_dtype == DT_F32 && out_dtype == DT_F32 && M % FT == 0 && N % FT == 0 && K % FK == 0 && aligned_lds) path = 1;
   if (force_path >= 0) {
@@ -49,15 +58,15 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
     // split-K only on the bf16 8-phase path (each slice an even number of 64-deep K-tiles); a request
     // that cannot be honoured (other kernel family / forced 2-stage variant) runs unsplit
     if (workspace == nullptr) return -1;
-    if (path == 0 && (K / BT_K) % (2 * ksplit) == 0 && g_bf16_variant != 1) {
+    if (path == 0 && (K / BT_K) % (2 * ksplit) == 0 && a.variant != 1) {
       a.ksplit = ksplit;
-      g_splitk_ws = workspace;
+      a.ws = workspace;
     }
   }
   if (mask != nullptr) {
     // the bitmask lives in the 8-phase kernels' tile-native layout: both GEMMs of a pair must run them
     if ((epi != EPI_ACT && epi != EPI_DACT) || act != ACT_RELU || in_dtype != DT_BF16 || out_dtype != DT_BF16 ||
-        path != 0 || a.ksplit != 1 || K % (2 * BT_K) != 0 || g_bf16_variant == 1)
+        path != 0 || a.ksplit != 1 || K % (2 * BT_K) != 0 || a.variant == 1)
       return -2;
     a.mask = mask;
   }
@@ -86,40 +95,9 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
   return (int)e;
 }
 
-// select the bf16 main-loop variant (see launch_bf16); returns the previous value
-int dllm_gemm_set_variant(int v) {
-  const int old = g_bf16_variant;
-  g_bf16_variant = v;
-  return old;
-}
-
-// minimum blocks per CU of a persistent 8-phase grid (>= 1); returns the previous value
-int dllm_gemm_set_min_blocks_per_cu(int n) {
-  const int old = g_min_bpc;
-  g_min_bpc = n < 1 ? 1 : n;
-  return old;
-}
-
-// tiles per persistent 8-phase block (<= 1: one block per tile); returns the previous value
-int dllm_gemm_set_tiles_per_block(int t) {
-  const int old = g_tpb;
-  g_tpb = t < 1 ? 1 : t;
-  return old;
-}
-
-// ablation launcher (performance investigation only): TN layout, bf16 out, square problems
-int dllm_gemm_ablation(int abl, const void* A, const void* B, void* C, int n, void* stream) {
-  GemmArgs a = {};
-  a.A = A; a.B = B; a.C = C; a.lda = n; a.ldb = n; a.ldc = n; a.M = n; a.N = n; a.K = n;
-  a.alpha = 1.f; a.group_m = 4;
-  if (n % 256) return -1;
-  const int nb = (n / 256) * (n / 256);
-  return (int)launch_tn_ablation(abl, a, nb, (hipStream_t)stream);
-}
-
 // which kernel family dllm_gemm would pick (for tests / profiling labels)
 int dllm_gemm_path(int in_dtype, int out_dtype, int M, int N, int K, long lda, long ldb, long ldc) {
-  const bool al = (lda % 8 == 0) && (ldb % 8 == 0) && (ldc % 4 == 0);
+  const bool al = (lda % 8 == 0) && (ldb % 8 == 0) && (ldc % 4 == 0);  // (bases: checked per call)
   if (in_dtype == DT_BF16 && M % BT_M == 0 && N % BT_N == 0 && K % BT_K == 0 && al) return 0;
   if (in_dtype == DT_F32 && out_dtype == DT_F32 && M % FT == 0 && N % FT == 0 && K % FK == 0 && al) return 1;
   return 2;

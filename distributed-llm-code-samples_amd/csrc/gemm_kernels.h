@@ -50,8 +50,13 @@ struct GemmArgs {
   float* opt_v;
   // split-K: ksplit > 1 -> the main kernel writes fp32 partials C + split*M*ldc (C = workspace)
   int ksplit;
-  // tiles per block of a persistent 8-phase kernel (PERS instantiations only)
+  // tiles per block of a persistent 8-phase kernel (PERS instantiations only; set by grid_8ph)
   int tpb;
+  // per-call launch policy (no process-wide kernel state: concurrent GEMMs on different streams may differ)
+  int variant;   // bf16 main loop: 0 auto, 1 2-stage, 2 8-phase, 3 8-phase staggered, 4 4-phase staggered
+  int tpb_req;   // requested tiles per persistent block (<= 1: one block per tile)
+  int min_bpc;   // minimum blocks per CU of a persistent grid (2 when collectives overlap the GEMMs)
+  float* ws;     // split-K fp32 partial workspace (caller-owned, ksplit * M * N floats)
   // ReLU activation-gradient bitmask (nullable; 8-phase kernels, bf16 out, compile-time ReLU): EPI_ACT writes
   // bit (act(h) != 0) per output element, EPI_DACT reads it instead of aux.  Tile-native layout: 8 KiB per
   // 256x256 tile (tile = tm * tiles_n + tn), 16 B per thread -- the same element->lane map in both GEMMs.
@@ -744,9 +749,6 @@ __device__ __forceinline__ bf16x8_t read_mc_half(const DLLM_LDS char* tile, int 
     asm volatile("" ::: "memory");          \
   } while (0)
 
-// ABL (ablation builds only; 0 in production): bit0/1 force K-contiguous LOADS of A/B, bit2/3 force
-// K-contiguous fragment READS of A/B, independent of LAYOUT (wrong results, same work) -- isolates the
-// cost of MN-contiguous LDS-DMA patterns vs transposed ds_read_b64_tr_b16 fragment reads.
 // Fragment reads of the 8-phase kernel are inline asm: hipcc cannot prove that a ds_read does not
 // alias an in-flight LDS-DMA (global_load_lds) write and would drain the whole prefetch pipeline with
 // s_waitcnt vmcnt(0) before every phase's reads.  RAW/WAR ordering against the DMA is instead carried
@@ -785,14 +787,11 @@ __device__ __forceinline__ GemmArgs reload_args() {
     __builtin_amdgcn_sched_barrier(0);                    \
   } while (0)
 
-// ABL (ablation builds only; 0 in production): bit0/1 force K-contiguous LOADS of A/B, bit2/3 force
-// K-contiguous fragment READS of A/B, independent of LAYOUT (wrong results, same work) -- isolates the
-// cost of MN-contiguous LDS-DMA patterns vs transposed ds_read_b64_tr_b16 fragment reads.
 // ACT >= 0: activation of the ACT/DACT/GLU/DGLU epilogues fixed at compile time (-1: runtime p.act)
 // NPH = 8: the 8-phase schedule below (one quadrant = 16 MFMAs per wave per barrier interval).
 // NPH = 4: half-tile phases (two quadrants = 32 MFMAs per interval, two half-tiles restaged per phase):
 // halves the barrier count per MFMA (see the NPH == 4 loop).
-template <int LAYOUT, int EPI, typename OutT, bool STAGGER, int ABL = 0, int ACT = -1, int NPH = 8, bool PERS = false>
+template <int LAYOUT, int EPI, typename OutT, bool STAGGER, int ACT = -1, int NPH = 8, bool PERS = false>
 __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
   // slot(op, hh, buf) = ((op*2 + hh)*2 + buf) * 16 KiB: A in [0, 64K), B in [64K, 128K), so every
   // fragment read is base + a 16-bit immediate
@@ -824,10 +823,10 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
     tm0 = (first_m + (bid % width) % gsz) * BT_M;
     tn0 = ((bid % width) / gsz) * BT_N;
   };
-  constexpr bool A_KC = (ABL & 1) ? true : (LAYOUT != L_TN);
-  constexpr bool B_KC = (ABL & 2) ? true : (LAYOUT == L_NT);
-  constexpr bool A_RKC = (ABL & 4) ? true : (LAYOUT != L_TN);
-  constexpr bool B_RKC = (ABL & 8) ? true : (LAYOUT == L_NT);
+  constexpr bool A_KC = (LAYOUT != L_TN);
+  constexpr bool B_KC = (LAYOUT == L_NT);
+  constexpr bool A_RKC = A_KC;  // fragment reads follow the operand image: ds_read_b128 / ds_read_b64_tr_b16
+  constexpr bool B_RKC = B_KC;
   uint32_t aoff[2], boff[2];
   if constexpr (A_KC) kc_half_offsets(p.lda, wid, lane, aoff); else mc_half_offsets(p.lda, wid, lane, aoff);
   if constexpr (B_KC) kc_half_offsets(p.ldb, wid, lane, boff); else mc_half_offsets(p.ldb, wid, lane, boff);
@@ -1387,20 +1386,6 @@ __global__ __launch_bounds__(256) void splitk_reduce(GemmArgs p, const float* ws
   }
 }
 
-// variant: 0 = auto (8-phase staggered when K % 128 == 0, else 2-stage), 1 = 2-stage, 2 = 8-phase, 3 = 8-phase staggered,
-// 4 = 4-phase (half-tile phases) staggered
-inline int g_bf16_variant = 0;
-// Persistent 8-phase blocks (the FFN's hot GEMMs): a block runs up to g_tpb output tiles back to back, the next
-// tile's first K-tiles prefetched under the current tile's epilogue (no pipeline drain, no block relaunch per
-// tile).  g_tpb <= 1: one block per tile.  The grid never drops below one block per CU, so g_tpb is capped at
-// tiles / CUs; at the default of 2 a block delayed by a concurrent kernel (an overlapped RCCL collective)
-// holds back at most two tiles.
-inline int g_tpb = 2;
-// Minimum blocks per CU of a persistent grid.  1 on a single device; 2 when collectives run concurrently
-// (set by the engine): an RCCL kernel holding a CU then delays one of >= 2 blocks per CU, whose tiles the
-// other CUs' later blocks absorb, instead of the only block of that CU (which would add a whole block's
-// time to the GEMM).
-inline int g_min_bpc = 1;
 constexpr int MAX_DEV = 64;
 inline int g_num_cu[MAX_DEV] = {};
 
@@ -1420,8 +1405,8 @@ static int num_cu() {
 static int grid_8ph(GemmArgs& a, int nb) {
   a.tpb = 1;
   const int ncu = num_cu();
-  if (g_tpb <= 1 || ncu <= 0) return nb;
-  const int t = std::min(g_tpb, nb / (ncu * std::max(1, g_min_bpc)));
+  if (a.tpb_req <= 1 || ncu <= 0) return nb;
+  const int t = std::min(a.tpb_req, nb / (ncu * std::max(1, a.min_bpc)));
   if (t <= 1) return nb;
   const int g = ((nb + t - 1) / t + 7) / 8 * 8;
   if (g >= nb) return nb;
@@ -1439,7 +1424,7 @@ static hipError_t launch_splitk(const GemmArgs& a, int out_dt, float* ws, hipStr
   w.beta = 0.f;
   const int nb = (a.M / BT_M) * (a.N / BT_N) * a.ksplit;
   w.tpb = 1;
-  if (g_bf16_variant == 4) hipLaunchKernelGGL((gemm_bf16_8ph<L, EPI_STORE, float, true, 0, -1, 4>), dim3(nb), dim3(512), 0, s, w);
+  if (a.variant == 4) hipLaunchKernelGGL((gemm_bf16_8ph<L, EPI_STORE, float, true, -1, 4>), dim3(nb), dim3(512), 0, s, w);
   else hipLaunchKernelGGL((gemm_bf16_8ph<L, EPI_STORE, float, true>), dim3(nb), dim3(512), 0, s, w);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
@@ -1453,8 +1438,6 @@ static hipError_t launch_splitk(const GemmArgs& a, int out_dt, float* ws, hipStr
 // ----------------------------------------------------------------------------------------------
 // host dispatch
 // ----------------------------------------------------------------------------------------------
-
-inline float* g_splitk_ws = nullptr;  // set per call by dllm_gemm (caller-owned workspace)
 
 // staggered 8-phase launch; the FFN's own activation epilogues (NT act/glu forward, NN dact/dglu
 // dgrad, bf16 out) get a compile-time activation, everything else the runtime switch
@@ -1476,11 +1459,11 @@ static void launch_8ph_act(const GemmArgs& a0, int nb0, hipStream_t s) {
     GemmArgs a = a0;
     const int nb = grid_8ph(a, nb0);
     if (a.tpb > 1) {
-      hipLaunchKernelGGL((gemm_bf16_8ph<L, E, OutT, true, 0, ACT, NPH, true>), dim3(nb), dim3(512), 0, s, a);
+      hipLaunchKernelGGL((gemm_bf16_8ph<L, E, OutT, true, ACT, NPH, true>), dim3(nb), dim3(512), 0, s, a);
       return;
     }
   }
-  hipLaunchKernelGGL((gemm_bf16_8ph<L, E, OutT, true, 0, ACT, NPH>), dim3(nb0), dim3(512), 0, s, a0);
+  hipLaunchKernelGGL((gemm_bf16_8ph<L, E, OutT, true, ACT, NPH>), dim3(nb0), dim3(512), 0, s, a0);
 }
 
 template <int L, int E, typename OutT, int NPH>
@@ -1500,9 +1483,9 @@ static void launch_8ph_stagger(const GemmArgs& a, int nb, hipStream_t s) {
 
 template <int L, int E>
 static hipError_t launch_bf16(const GemmArgs& a, int out_dt, hipStream_t s) {
-  if (a.ksplit > 1) return launch_splitk<L, E>(a, out_dt, g_splitk_ws, s);
+  if (a.ksplit > 1) return launch_splitk<L, E>(a, out_dt, a.ws, s);
   const int nb = (a.M / BT_M) * (a.N / BT_N);
-  int v = g_bf16_variant;
+  int v = a.variant;
   if (v == 0) v = (a.K % (2 * BT_K) == 0) ? 3 : 1;
   if (v >= 2 && a.K % (2 * BT_K) != 0) v = 1;
   const bool f32 = out_dt == DT_F32;
@@ -1562,12 +1545,12 @@ static hipError_t dispatch_epi(int path, int epi, const GemmArgs& a, int in_dt, 
 // weight-gradient GEMMs with a fused optimizer epilogue: TN layout, fp32 master output only
 template <int E>
 static hipError_t dispatch_opt(int path, const GemmArgs& a, int in_dt, hipStream_t s) {
-  if (path == 0 && a.ksplit > 1) return launch_splitk<L_TN, E>(a, DT_F32, g_splitk_ws, s);
+  if (path == 0 && a.ksplit > 1) return launch_splitk<L_TN, E>(a, DT_F32, a.ws, s);
   if (path == 0) {
     const int nb = (a.M / BT_M) * (a.N / BT_N);
-    if (a.K % (2 * BT_K) == 0 && g_bf16_variant == 4)
-      hipLaunchKernelGGL((gemm_bf16_8ph<L_TN, E, float, true, 0, -1, 4>), dim3(nb), dim3(512), 0, s, a);
-    else if (a.K % (2 * BT_K) == 0 && g_bf16_variant != 1)
+    if (a.K % (2 * BT_K) == 0 && a.variant == 4)
+      hipLaunchKernelGGL((gemm_bf16_8ph<L_TN, E, float, true, -1, 4>), dim3(nb), dim3(512), 0, s, a);
+    else if (a.K % (2 * BT_K) == 0 && a.variant != 1)
       launch_8ph_act<L_TN, E, float, -1, 8>(a, nb, s);
     else
       hipLaunchKernelGGL((gemm_bf16_256<L_TN, E, float>), dim3(nb), dim3(512), 0, s, a);
@@ -1586,6 +1569,5 @@ hipError_t dispatch_nt(int path, int epi, const GemmArgs& a, int in_dt, int out_
 hipError_t dispatch_nn(int path, int epi, const GemmArgs& a, int in_dt, int out_dt, hipStream_t s);
 hipError_t dispatch_tn(int path, int epi, const GemmArgs& a, int in_dt, int out_dt, hipStream_t s);
 hipError_t dispatch_tn_opt(int path, int epi, const GemmArgs& a, int in_dt, hipStream_t s);
-hipError_t launch_tn_ablation(int abl, const GemmArgs& a, int nb, hipStream_t s);
 
 }  // namespace dllm

@@ -28,6 +28,7 @@ from __future__ import annotations
 import torch
 
 from .. import _native
+from ..utils import observe as _observe
 from .activations import act_code, act_fwd, act_grad
 
 LAYOUTS = {"nt": 0, "nn": 1, "tn": 2}
@@ -158,17 +159,23 @@ def set_splitk(enabled: bool) -> bool:
     return old
 
 
-_LIBRARY_PLAIN_NT = {"enabled": False}
 _VARIANT = {"name": "auto"}
+# Launch policy of the 256x256 bf16 kernels (tiles per persistent block, minimum blocks per CU): Python-level
+# defaults that every call passes to the library explicitly -- the native side keeps no mutable state, so
+# GEMMs issued concurrently on different streams never race on a setting.
+_POLICY = {"tpb": 2, "min_bpc": 1}
+# split-K fp32 partial workspaces, cached per (device, stream): a GEMM only ever reuses its own stream's
+# buffer, so stream order serialises the reuse
+_WS: dict = {}
 
 
-def set_library_plain_nt(enabled: bool) -> bool:
-    """Route PLAIN NT GEMMs (store epilogue, alpha 1, beta 0, bf16 in and out — the forward ``y = a·W2ᵀ``)
-    to hipBLASLt through ``torch.matmul``.  Every fused GEMM (activation, mask, gate, optimizer) and every
-    NN/TN GEMM stays on the native kernels.  Returns the previous setting."""
-    old = _LIBRARY_PLAIN_NT["enabled"]
-    _LIBRARY_PLAIN_NT["enabled"] = bool(enabled)
-    return old
+def _splitk_workspace(numel: int, device: torch.device) -> torch.Tensor:
+    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
+    ws = _WS.get(key)
+    if ws is None or ws.numel() < numel:
+        ws = torch.empty(numel, dtype=torch.float32, device=device)
+        _WS[key] = ws
+    return ws
 
 
 def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None = None, *, epi: str = "store",
@@ -206,9 +213,6 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
 
     for t, nm in ((a, "a"), (b, "b"), (out, "out")):
         _check_rowmajor(t, nm)
-    if (_LIBRARY_PLAIN_NT["enabled"] and layout == "nt" and epi == "store" and alpha == 1.0 and beta == 0.0
-            and force is None and a.dtype == torch.bfloat16 and out.dtype == torch.bfloat16):
-        return torch.matmul(a, b.t(), out=out)
     auxt = aux if aux is not None else aux_out
     if auxt is not None:
         _check_rowmajor(auxt, "aux")
@@ -223,9 +227,12 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
     if a.dtype == torch.bfloat16 and force in (None, "mfma_bf16"):
         ksplit = choose_ksplit(M, N, K)
         if ksplit > 1 and L.dllm_gemm_path(in_dt, out_dt, M, N, K, a.stride(0), b.stride(0), out.stride(0)) == 0:
-            ws = torch.empty(ksplit * M * N, dtype=torch.float32, device=a.device)
+            ws = _splitk_workspace(ksplit * M * N, a.device)
         else:
             ksplit = 1
+    obs = _observe.active()
+    if obs is not None:
+        obs.gemm_begin()
     rc = L.dllm_gemm(in_dt, out_dt, LAYOUTS[layout], EPIS[epi], act_code(act),
                      a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), out.data_ptr(), out.stride(0),
                      aux.data_ptr() if aux is not None else None,
@@ -236,8 +243,11 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
                      float(wd), int(step), opt_m.data_ptr() if opt_m is not None else None,
                      opt_v.data_ptr() if opt_v is not None else None, ksplit,
                      ws.data_ptr() if ws is not None else None,
-                     _mask_ptr(mask, M, N) if mask is not None else None)
+                     _mask_ptr(mask, M, N) if mask is not None else None,
+                     BF16_VARIANTS[_VARIANT["name"]], _POLICY["tpb"], _POLICY["min_bpc"])
     _native.check(rc, f"dllm_gemm({layout},{epi},M={M},N={N},K={K})")
+    if obs is not None:
+        obs.gemm_end()
     return out
 
 
@@ -263,25 +273,31 @@ BF16_VARIANTS = {"auto": 0, "2stage": 1, "8phase": 2, "8phase_stagger": 3, "4pha
 
 
 def set_bf16_variant(name: str) -> str:
-    """Select the bf16 256x256 main loop (process-wide); returns the previous setting's name."""
-    old = _native.lib().dllm_gemm_set_variant(BF16_VARIANTS[name])
+    """Select the bf16 256x256 main loop for subsequent calls; returns the previous setting's name."""
+    if name not in BF16_VARIANTS:
+        raise ValueError(f"unknown bf16 GEMM variant {name!r}")
+    old = _VARIANT["name"]
     _VARIANT["name"] = name
-    return {v: k for k, v in BF16_VARIANTS.items()}[old]
+    return old
 
 
 def set_tiles_per_block(n: int) -> int:
-    """Persistent 8-phase GEMM blocks (process-wide) for the FFN's own GEMMs: each block runs up to ``n``
-    output tiles back to back, the next tile's first K-tiles prefetched while the current tile's epilogue
-    runs (no pipeline drain or block relaunch per tile).  Capped at tiles / CUs so every CU keeps a block;
-    ``n <= 1``: one block per tile.  Default 2.  Returns the previous setting."""
-    return int(_native.lib().dllm_gemm_set_tiles_per_block(int(n)))
+    """Persistent 8-phase GEMM blocks for the FFN's own GEMMs: each block runs up to ``n`` output tiles back to
+    back, the next tile's first K-tiles prefetched while the current tile's epilogue runs (no pipeline drain or
+    block relaunch per tile).  Capped at tiles / CUs so every CU keeps a block; ``n <= 1``: one block per tile.
+    Default 2.  Returns the previous setting."""
+    old = _POLICY["tpb"]
+    _POLICY["tpb"] = max(1, int(n))
+    return old
 
 
 def set_min_blocks_per_cu(n: int) -> int:
-    """Minimum blocks per CU of a persistent GEMM grid (process-wide; default 1).  The engine sets 2 when
-    collectives run concurrently with the GEMMs, so a CU held by an RCCL kernel delays one of several blocks
-    per CU rather than the only one.  Returns the previous setting."""
-    return int(_native.lib().dllm_gemm_set_min_blocks_per_cu(int(n)))
+    """Minimum blocks per CU of a persistent GEMM grid (default 1).  The engine sets 2 when collectives run
+    concurrently with the GEMMs, so a CU held by an RCCL kernel delays one of several blocks per CU rather than
+    the only one.  Returns the previous setting."""
+    old = _POLICY["min_bpc"]
+    _POLICY["min_bpc"] = max(1, int(n))
+    return old
 
 
 def gemm_path(a_dtype: torch.dtype, out_dtype: torch.dtype, M: int, N: int, K: int,

@@ -99,6 +99,8 @@ class CustomAllReduce:
         nbytes = t.numel() * t.element_size()
         if nbytes % 16 or nbytes > self.cap:
             raise ValueError(f"custom all-reduce: {nbytes} B (needs a multiple of 16, <= {self.cap})")
+        if t.data_ptr() % 16:
+            raise ValueError("custom all-reduce: the tensor must be 16-byte aligned (uint4 copies)")
         s = stream.cuda_stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream
         _native.check(_native.lib().dllm_car_all_reduce(self.st, t.data_ptr(), nbytes, _DT[t.dtype], self.timeout_s, s),
                       "dllm_car_all_reduce")

@@ -19,6 +19,8 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
+from ..utils import observe
+
 
 class Done:
     """Completed-work placeholder (single-rank groups, or nothing to do)."""
@@ -62,19 +64,31 @@ def _active(group) -> bool:
     return group is not None and dist.is_initialized()
 
 
+def _issue(group, fn):
+    """Run ``fn()`` (which issues one collective and returns its work); with a ``CommObserver`` active the
+    collective's issue and completion are recorded (utils/observe.py)."""
+    obs = observe.active()
+    if obs is None:
+        return fn()
+    ev = obs.issue()
+    w = fn()
+    obs.issued(group, ev, w)
+    return w
+
+
 def all_reduce(t: torch.Tensor, group, async_op: bool = True):
     if group is not None and _native(group):
-        w = group.all_reduce(t)
+        w = _issue(group, lambda: group.all_reduce(t))
         return _finish(w, async_op) if (async_op or _SERIALIZE) else (w.wait(), Done())[1]
     if not _active(group):
         return Done()
-    w = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=True)
+    w = _issue(group, lambda: dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=True))
     return _finish(w, async_op) if (async_op or _SERIALIZE) else (w.wait(), Done())[1]
 
 
 def all_gather_into(out: torch.Tensor, shard: torch.Tensor, group, async_op: bool = True):
     if group is not None and _native(group):
-        w = group.all_gather_into(out.view(-1), shard.reshape(-1))
+        w = _issue(group, lambda: group.all_gather_into(out.view(-1), shard.reshape(-1)))
         return _finish(w, async_op) if (async_op or _SERIALIZE) else (w.wait(), Done())[1]
     if not _active(group):
         if out.data_ptr() != shard.data_ptr():
@@ -83,13 +97,14 @@ def all_gather_into(out: torch.Tensor, shard: torch.Tensor, group, async_op: boo
     n = dist.get_world_size(group)
     if out.numel() != shard.numel() * n:
         raise ValueError(f"all_gather_into: out {out.numel()} != {n} x shard {shard.numel()}")
-    w = dist.all_gather_into_tensor(out.view(-1), shard.reshape(-1), group=group, async_op=True)
+    w = _issue(group, lambda: dist.all_gather_into_tensor(out.view(-1), shard.reshape(-1), group=group,
+                                                         async_op=True))
     return _finish(w, async_op) if (async_op or _SERIALIZE) else (w.wait(), Done())[1]
 
 
 def reduce_scatter_into(out: torch.Tensor, full: torch.Tensor, group, async_op: bool = True):
     if group is not None and _native(group):
-        w = group.reduce_scatter_into(out.view(-1), full.reshape(-1))
+        w = _issue(group, lambda: group.reduce_scatter_into(out.view(-1), full.reshape(-1)))
         return _finish(w, async_op) if (async_op or _SERIALIZE) else (w.wait(), Done())[1]
     if not _active(group):
         if out.data_ptr() != full.data_ptr():
@@ -98,8 +113,8 @@ def reduce_scatter_into(out: torch.Tensor, full: torch.Tensor, group, async_op: 
     n = dist.get_world_size(group)
     if full.numel() != out.numel() * n:
         raise ValueError(f"reduce_scatter_into: full {full.numel()} != {n} x out {out.numel()}")
-    w = dist.reduce_scatter_tensor(out.view(-1), full.reshape(-1), op=dist.ReduceOp.SUM, group=group,
-                                   async_op=True)
+    w = _issue(group, lambda: dist.reduce_scatter_tensor(out.view(-1), full.reshape(-1), op=dist.ReduceOp.SUM,
+                                                        group=group, async_op=True))
     return _finish(w, async_op) if (async_op or _SERIALIZE) else (w.wait(), Done())[1]
 
 

@@ -739,7 +739,16 @@ class FFNTrainer:
         elif not self.fused_opt and not self.side_opt:
             self._opt(0, self.total)
         self._unmark(mark)
+        if cfg.debug_sync:
+            self.check_health()
         return y
+
+    def check_health(self) -> None:
+        """Raise if an asynchronous failure was recorded on the device: a timed-out barrier of the custom
+        TP all-reduce (whose results are then NaN-poisoned, csrc/car.hip).  Synchronises the device; called
+        after every step under ``debug_sync`` and by the drivers after their final synchronize."""
+        if self.tp_car is not None:
+            self.tp_car.check()
 
     # ------------------------------------------------------------------------------------------------
     # phase annotation: roctx ranges (DLLM_ROCTX=1, rocprofv3 --marker-trace) and optional HIP-event

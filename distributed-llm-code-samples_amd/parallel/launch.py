@@ -120,6 +120,7 @@ def run_rank(rank: int, world: int, cfg_dict: dict, method: int, backend: str, p
         mesh.destroy(abort=True)
         raise
     timer.finish()
+    eng.check_health()
     if opts.get("ckpt_dir"):
         save_checkpoint(eng, opts["ckpt_dir"], step=done, fmt=opts.get("ckpt_format", "consolidated"),
                         meta={"method": method, "seed": seed, "cfg": cfg_dict})

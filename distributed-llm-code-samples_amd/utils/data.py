@@ -85,8 +85,10 @@ class CpuCompatData:
     def fill(self, seed: int, next_seed: int | None = None) -> tuple[torch.Tensor, torch.Tensor]:
         fut = self._pending.pop(int(seed), None)
         x, dy = fut.result() if fut is not None else self._draw(seed)
-        if self.pin and self._host is not None:
-            torch.cuda.current_stream(self.device).synchronize()  # previous pinned buffers no longer in use
+        # no host synchronisation: the device buffers are reused in stream order, and a pinned host batch
+        # released here goes back to torch's caching host allocator, which records an event on the stream
+        # of every non_blocking copy out of it and reuses the block only after that event -- so the host
+        # keeps enqueueing ahead of the GPU instead of waiting for the previous step
         self.x.copy_(x, non_blocking=self.pin)
         self.dy.copy_(dy, non_blocking=self.pin)
         self._host = (x, dy)

@@ -5,8 +5,8 @@ single-device / TP-free path once, then replays it: one ``hipGraphLaunch`` per s
 launches through Python.  The per-step data seed lives in device memory (``rng_normal_devseed_``), so each
 replay draws new data; everything else is static (preallocated flat buffers, fixed shapes).
 
-Restrictions (checked): no gradient collectives (``eng.fused_opt`` path) and SGD (AdamW's bias
-correction is a per-step kernel argument).
+Restrictions (checked): no gradient collectives (``eng.fused_opt`` path), SGD (AdamW's bias correction is a
+per-step kernel argument) and no concurrent weight-gradient stream.
 """
 from __future__ import annotations
 
@@ -22,6 +22,10 @@ class GraphedStep:
             raise ValueError("graph capture needs a GPU engine")
         if not eng.fused_opt or eng.cfg.optimizer != "sgd" or eng.mesh.world > 1:
             raise ValueError("GraphedStep supports the single-device fused-SGD path only")
+        if eng.wg_stream is not None:
+            # the concurrent weight-gradient stream carries Python-side events across steps (da/dx buffer
+            # reuse), which a replayed capture cannot re-record
+            raise ValueError("GraphedStep does not support the concurrent weight-gradient stream (wgrad_stream)")
         self.eng = eng
         dev = eng.device
         self.seed = torch.zeros(1, dtype=torch.int64, device=dev)

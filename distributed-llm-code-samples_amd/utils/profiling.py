@@ -4,7 +4,8 @@ Reference: the ``torch_profile_rank_0`` decorator (train_ffns.py:129-141) wraps 
 ``torch.profiler.profile(CPU+CUDA, record_shapes, with_stack)`` and exports ``trace_profiler_trace.json``
 on rank 0; it rebinds a module-level ``global`` so ``spawn`` can pickle it, which breaks when applied to
 a second function.  Here profiling is a context manager (nothing to pickle) and
-kernel-level evidence comes from ``rocprofv3 --kernel-trace --stats`` (scripts/profile.sh).
+kernel-level evidence comes from ``rocprofv3 --kernel-trace --stats`` (``profiles/README.md`` lists the
+commands; ``scripts/rocpd_stats.py`` summarises a run's database).
 """
 from __future__ import annotations
 

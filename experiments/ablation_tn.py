@@ -1,4 +1,8 @@
-"""TN GEMM ablation: MN-contiguous LDS-DMA loads vs transposed fragment reads (8192^3, bf16)."""
+"""TN GEMM ablation: MN-contiguous LDS-DMA loads vs transposed fragment reads (8192^3, bf16).
+
+Historical (round 1, evidence for profiles/ablation_tn_r1_after.log): needs the ablation build of the GEMM
+library at commit e72e569 (the ``ABL`` template parameter and ``dllm_gemm_ablation`` were removed from the
+production library), loaded through ``DLLM_NATIVE_LIB=<path to that build>``."""
 import os, sys, statistics
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch

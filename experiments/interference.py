@@ -1,9 +1,10 @@
 """How much do CU-occupying side-stream kernels (a stand-in for RCCL channel workgroups during an
 overlapped collective) slow the GEMMs down?
 
-    python scripts/interference.py [--cus 0,8,16,32,64] [--usec 3000]
+    python experiments/interference.py [--cus 0,8,16,32,64] [--usec 3000]
 
-A side stream keeps `c` CUs busy (dllm_occupy_cus: one 96-KiB-LDS wave per CU, spinning) for the whole
+A side stream keeps `c` CUs busy (experiments/occupy.hip, built here into its own .so: one 96-KiB-LDS wave per CU,
+spinning) for the whole
 timed window while the main stream runs a GEMM back to back.  The ideal slowdown is 256/(256-c); anything
 above that is tile-wave quantisation / dispatch interference.  Also reports torch.matmul (hipBLASLt).
 """
@@ -11,16 +12,26 @@ import argparse
 import ctypes
 import json
 import os
+import subprocess
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 import dllm  # noqa: E402,F401
-from dllm import _native  # noqa: E402
 from dllm.ops.gemm import gemm  # noqa: E402
 
-_native.register_optional("dllm_occupy_cus", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_void_p])
+
+
+def _occupier() -> ctypes.CDLL:
+    here = os.path.dirname(os.path.abspath(__file__))
+    src, so = os.path.join(here, "occupy.hip"), os.path.join(here, "_occupy.so")
+    if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
+        subprocess.run(["hipcc", "-O3", "-fPIC", "-shared", "--offload-arch=gfx950", src, "-o", so], check=True)
+    lib = ctypes.CDLL(so)
+    lib.dllm_occupy_cus.restype = ctypes.c_int
+    lib.dllm_occupy_cus.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    return lib
 
 
 def main():
@@ -38,6 +49,7 @@ def main():
 
     set_tiles_per_block(a.tpb)
     set_min_blocks_per_cu(a.min_bpc)
+    occ = _occupier()
     T, D, F = a.T, a.D, a.F
     bf, dev = torch.bfloat16, "cuda"
     x = torch.randn(T, D, device=dev, dtype=bf)
@@ -54,7 +66,6 @@ def main():
         "wgrad TN bf16 (1024 tiles)": lambda: gemm(dy, h, "tn", out=g),
         "dx-shape NN (512 tiles)": lambda: gemm(h, w1, "nn", out=out_td),
     }
-    lib = _native.lib()
     side = torch.cuda.Stream()
     res = {}
     for name, fn in cases.items():
@@ -66,7 +77,7 @@ def main():
             # estimate the window: iters * ~1.5 ms, cover it generously
             if c:
                 with torch.cuda.stream(side):
-                    rc = lib.dllm_occupy_cus(c, 2000 + 2000 * a.iters, side.cuda_stream)
+                    rc = occ.dllm_occupy_cus(c, 2000 + 2000 * a.iters, side.cuda_stream)
                     assert rc == 0, rc
                 torch.cuda._sleep(2_000_000)  # let the occupiers land before the GEMMs start
             s.record()

@@ -1,0 +1,50 @@
+"""Summarise a rocprofv3 rocpd database (``-d DIR -o run`` -> ``DIR/run_results.db``): per-kernel totals, plus
+a steady-state timeline of the last step(s).
+
+    python scripts/rocpd_stats.py gpurun_out/prof/run_results.db [--last_ms 30.6] [--timeline N]
+
+``--last_ms``: also print every dispatch of the final window of that length (one step), with gaps."""
+import argparse
+import collections
+import sqlite3
+
+
+def short(n: str, w: int = 88) -> str:
+    n = n.replace("void ", "").replace("dllm::", "")
+    return n[:w]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("db")
+    ap.add_argument("--last_ms", type=float, default=0.0)
+    ap.add_argument("--top", type=int, default=25)
+    a = ap.parse_args()
+    c = sqlite3.connect(a.db)
+    rows = c.execute("select name, start, end, grid_x, workgroup_x from kernels order by start").fetchall()
+    agg = collections.defaultdict(lambda: [0, 0])
+    for n, s, e, *_ in rows:
+        agg[n][0] += 1
+        agg[n][1] += e - s
+    tot = sum(v[1] for v in agg.values())
+    print(f"{'kernel':88s} {'calls':>6s} {'avg_us':>9s} {'total_ms':>9s} {'%':>6s}")
+    for n, (k, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:a.top]:
+        print(f"{short(n):88s} {k:6d} {t / k / 1e3:9.1f} {t / 1e6:9.2f} {100 * t / tot:6.2f}")
+    print(f"total kernel time {tot / 1e6:.2f} ms over {len(rows)} dispatches")
+    if a.last_ms > 0 and rows:
+        t1 = max(r[2] for r in rows)
+        cut = t1 - a.last_ms * 1e6
+        win = [r for r in rows if r[1] >= cut]
+        busy, last = 0, 0
+        print(f"\nlast {a.last_ms} ms window: {len(win)} dispatches")
+        for n, s, e, gx, wx in win:
+            gap = (s - last) / 1e3 if last else 0.0
+            print(f"  +{(s - win[0][1]) / 1e3:9.1f} us  {(e - s) / 1e3:8.1f} us  gap {gap:7.1f}  grid {gx // max(wx, 1):6d}  {short(n, 70)}")
+            busy += max(0, e - max(s, last))
+            last = max(last, e)
+        span = win[-1][2] - win[0][1]
+        print(f"window span {span / 1e6:.2f} ms, busy {busy / 1e6:.2f} ms ({100 * busy / span:.1f}%)")
+
+
+if __name__ == "__main__":
+    main()

@@ -104,7 +104,10 @@ def _proc(rank, world, port, kind, shards, seeds):
 
     os.environ["MASTER_PORT"] = str(port)
     fn = {"ddp": api.train_process_ddp, "fsdp": api.train_process_fsdp, "tp": api.train_process_tp}[kind]
-    api.init_process(rank, shards[rank], seeds, T, D, fn, world_size=world, backend="gloo")
+    # like the reference's drivers: DDP/FSDP workers get their own stripe (cpus_seeds[rank], train_ffns.py:182,
+    # :273), TP workers every seed (:324)
+    mine = seeds if kind == "tp" else seeds.reshape(-1, world)[:, rank]
+    api.init_process(rank, shards[rank], mine, T, D, fn, world_size=world, backend="gloo")
     import torch.distributed as dist
 
     dist.destroy_process_group()

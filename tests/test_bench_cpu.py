@@ -11,12 +11,12 @@ KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "
         "vs_baseline", "dtype", "data", "config"}
 
 
-@pytest.mark.parametrize("method", ["zero", "ddp", "fsdp", "tp"])
-def test_bench_torchrun_gloo_two_ranks(method, free_port):
+def _run(free_port, *extra):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port), os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--steps", "2", "--warmup", "1", "--backend", "gloo", "--method", method,
-           "--model_size", "64", "--layers", "2", "--batch_size", "2", "--seq_len", "16", "--dtype", "fp32"]
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--backend", "gloo",
+           "--model_size", "64", "--layers", "2", "--batch_size", "2", "--seq_len", "16", "--dtype", "fp32",
+           "--mp_ffn_dim", "128", *extra]
     env = dict(os.environ, PYTHONPATH=ROOT)
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
@@ -24,4 +24,26 @@ def test_bench_torchrun_gloo_two_ranks(method, free_port):
     assert len(lines) == 1, r.stdout
     rec = json.loads(lines[0])
     assert KEYS <= set(rec) and rec["value"] > 0 and rec["finite"]
+    return rec
+
+
+@pytest.mark.parametrize("method", ["ddp", "fsdp", "tp"])
+def test_bench_torchrun_gloo_two_ranks(method, free_port):
+    rec = _run(free_port, "--method", method, "--methods", "none")
     assert rec["config"]["global_batch"] == (2 if method == "tp" else 4)
+    assert "methods" not in rec
+    if method == "tp":
+        assert "F128" in rec["config"]["model"] and rec["scaling"] == "strong"  # the MP config's FFN width
+
+
+def test_bench_methods_side_by_side(free_port):
+    """The default run: ZeRO-2 headline plus ddp / zero / fsdp / tp timed side by side on their own engines
+    (the reference's --method 0, train_ffns.py:373-384)."""
+    rec = _run(free_port)
+    assert rec["config"]["parallelism"] == "dp2-zero2" and rec["config"]["global_batch"] == 4
+    assert set(rec["methods"]) == {"ddp", "zero", "fsdp", "tp"}
+    for name, m in rec["methods"].items():
+        assert m["value"] > 0 and m["ms_per_step"] > 0 and m["finite"], name
+        assert {"peak_hbm_gib", "parallelism", "model", "state_gib"} <= set(m), name
+    assert rec["methods"]["tp"]["parallelism"] == "tp2" and "L1 D64 F128" in rec["methods"]["tp"]["model"]
+    assert rec["methods"]["fsdp"]["parallelism"] == "fsdp2"

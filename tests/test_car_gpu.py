@@ -128,3 +128,48 @@ def test_tp_engine_with_custom_allreduce(free_port):
             d_got = got.double() - layers[l][k].double()
             d_want = want[l][k].double() - layers[l][k].double()
             assert (d_got - d_want).norm() / d_want.norm() < 2e-3, (l, k)
+
+
+def _stall_proc(rank, n, port, q):
+    import torch.distributed as dist
+
+    from dllm.parallel.car import CustomAllReduce
+
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=n)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    car = CustomAllReduce(list(range(n)), dev, cap_bytes=4096 * 4, tag="stall", timeout_s=0.5)
+    res = None
+    if rank == 0:  # rank 1 stalls: it never enters the all-reduce
+        t = torch.ones(4096, device=dev)
+        car.all_reduce(t)
+        try:
+            car.check()
+            res = "no error"
+        except RuntimeError as e:
+            res = ("raised", "timed out" in str(e), bool(torch.isnan(t).all().item()))
+        car.all_reduce(t)  # a later call fails fast (no second spin) and stays poisoned
+        torch.cuda.synchronize()
+        res = res + (bool(torch.isnan(t).all().item()),)
+    dist.barrier()
+    car.destroy()
+    dist.barrier()
+    dist.destroy_process_group()
+    q.put((rank, res))
+
+
+def test_stalled_peer_fails_loudly(free_port):
+    """A peer that never arrives: the bounded barrier times out, the result is NaN-poisoned (never a
+    silently partial sum) and ``check()`` -- which the engine runs at its sync points -- raises."""
+    n = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_stall_proc, args=(r, n, free_port, q)) for r in range(n)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(n))
+    for p in ps:
+        p.join(60)
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+    assert res[0] == ("raised", True, True, True), res[0]
