@@ -162,8 +162,34 @@ class FFNTrainer:
                 self.entries.append(e)
         self.total = off
         self.entry = {(e.layer, e.name): e for e in self.entries}
-        self.master = torch.zeros(self.total, dtype=torch.float32, device=dev)
-        self.shared_copy = self.cd == torch.float32
+        self._entry_index = {(e.layer, e.name): i for i, e in enumerate(self.entries)}
+
+        # ---- DDP / ZeRO buckets ------------------------------------------------------------------
+        self.buckets = []  # (start, end, last_entry_index)
+        if self.ddp or self.zero:
+            esize = torch.empty(0, dtype=self.gd).element_size()
+            cap = int(cfg.bucket_mb * 2**20 / esize) if cfg.bucket_mb > 0 else 0
+            start = 0
+            for i, e in enumerate(self.entries):
+                end = e.offset + _round_up(e.numel, self.align)
+                if cap == 0 or end - start >= cap or i == len(self.entries) - 1:
+                    self.buckets.append((start, end, i))
+                    start = end
+        if self.zero:
+            # rank r owns [s + r*(e-s)/d, s + (r+1)*(e-s)/d) of every bucket; the owned pieces of all buckets
+            # are stored back to back (shard offset goff): the fp32 master, the Adam moments and the reduced
+            # gradient exist ONLY for the owned 1/dp (ZeRO-2), the compute copy stays full (it is what the
+            # forward and backward read, refreshed by the per-bucket all-gather)
+            self.bucket_shard = []
+            goff = 0
+            for s_, e_, _ in self.buckets:
+                n = (e_ - s_) // d
+                self.bucket_shard.append((s_ + mesh.dp_rank * n, s_ + (mesh.dp_rank + 1) * n, goff))
+                goff += n
+            self.shard_total = goff
+        # ---- flat state ----------------------------------------------------------------------------
+        self.master = torch.zeros(self.shard_total if self.zero else self.total, dtype=torch.float32, device=dev)
+        self.shared_copy = self.cd == torch.float32 and not self.zero
         self.copy = self.master if self.shared_copy else torch.zeros(self.total, dtype=self.cd, device=dev)
         # no gradient collective (single device / pure TP): the optimizer runs inside the wgrad GEMMs and
         # no flat gradient buffer exists at all
@@ -177,8 +203,8 @@ class FFNTrainer:
             self.opt_stream_side = torch.cuda.Stream(device=dev)
             self.opt_done = {}
         if cfg.optimizer == "adam":
-            self.adam_m = torch.zeros(self.total, dtype=torch.float32, device=dev)
-            self.adam_v = torch.zeros(self.total, dtype=torch.float32, device=dev)
+            self.adam_m = torch.zeros(self.master.numel(), dtype=torch.float32, device=dev)
+            self.adam_v = torch.zeros(self.master.numel(), dtype=torch.float32, device=dev)
 
         # ---- FSDP rings --------------------------------------------------------------------------
         if self.fsdp:
@@ -229,16 +255,8 @@ class FFNTrainer:
             self.dyfull = torch.empty((T, D), dtype=self.cd, device=dev)
             self.dxs = [torch.empty((Tl, D), dtype=self.cd, device=dev) for _ in range(2)]
 
-        # ---- DDP / ZeRO buckets ------------------------------------------------------------------
-        self.buckets = []  # (start, end, last_entry_index)
+        # ---- DDP / ZeRO bucket state ----------------------------------------------------------------
         if self.ddp or self.zero:
-            cap = int(cfg.bucket_mb * 2**20 / self.grads.element_size()) if cfg.bucket_mb > 0 else 0
-            start = 0
-            for i, e in enumerate(self.entries):
-                end = e.offset + _round_up(e.numel, self.align)
-                if cap == 0 or end - start >= cap or i == len(self.entries) - 1:
-                    self.buckets.append((start, end, i))
-                    start = end
             self.bucket_work = [None] * len(self.buckets)
             self.weight_buckets = {(l, n): sorted(b for b, (s_, e_, _) in enumerate(self.buckets)
                                                   if s_ < self.entry[(l, n)].offset + self.entry[(l, n)].numel
@@ -249,18 +267,9 @@ class FFNTrainer:
             self.opt_stream = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
             self.ddp_done = [None] * len(self.buckets)
         if self.zero:
-            # rank r owns [s + r*(e-s)/d, s + (r+1)*(e-s)/d) of every bucket
-            self.gshard = torch.zeros(self.total // d, dtype=self.gd, device=dev)
-            self.bucket_shard = []
-            goff = 0
-            for s_, e_, _ in self.buckets:
-                n = (e_ - s_) // d
-                self.bucket_shard.append((s_ + mesh.dp_rank * n, s_ + (mesh.dp_rank + 1) * n, goff))
-                goff += n
+            self.gshard = torch.zeros(self.shard_total, dtype=self.gd, device=dev)
             self.ag_pending = [None] * len(self.buckets)
             self.rs_issued_at = [None] * len(self.buckets)
-            self._master_synced = True
-        self._entry_index = {(e.layer, e.name): i for i, e in enumerate(self.entries)}
         self._next_bucket = 0
 
     # ------------------------------------------------------------------------------------------------
@@ -270,7 +279,29 @@ class FFNTrainer:
         return flat[e.offset:e.offset + e.numel].view(e.shape)
 
     def master_view(self, l: int, name: str) -> torch.Tensor:
+        if self.zero:
+            raise RuntimeError("ZeRO keeps only this rank's shard of the fp32 master (see full_flat)")
         return self._view(self.master, self.entry[(l, name)])
+
+    def _owned_segments(self, lo: int, hi: int):
+        """ZeRO: the parts of flat range [lo, hi) this rank owns, as (flat_lo, flat_hi, shard_offset)."""
+        for ss, se, go in self.bucket_shard:
+            a, b = max(lo, ss), min(hi, se)
+            if a < b:
+                yield a, b, go + (a - ss)
+
+    @torch.no_grad()
+    def full_flat(self, shard: torch.Tensor) -> torch.Tensor:
+        """ZeRO: all-gather a shard-layout fp32 buffer (master / Adam moment) into a new full-layout flat
+        buffer (collective over dp; a transient -- nothing full-size is kept).  Other modes: returned as is."""
+        if not self.zero:
+            return shard
+        full = torch.zeros(self.total, dtype=shard.dtype, device=shard.device)
+        grp = self.mesh.group("dp_ag")
+        for b, (s_, e_, _) in enumerate(self.buckets):
+            ss, se, go = self.bucket_shard[b]
+            comm.all_gather_into(full[s_:e_], shard[go:go + (se - ss)].clone(), grp, async_op=False)
+        return full
 
     def copy_view(self, l: int, name: str) -> torch.Tensor:
         return self._view(self.copy, self.entry[(l, name)])
@@ -341,8 +372,8 @@ class FFNTrainer:
         return {"w1": w1, "w2": w2}
 
     def flat_buffers(self) -> dict:
-        """Named flat fp32 state buffers sharing the parameter layout (checkpointed).  Under ZeRO the
-        owned shards are all-gathered first so every buffer is complete on every rank (collective)."""
+        """Named flat fp32 state buffers as this rank stores them (checkpointed): full layout, FSDP row
+        shards, or the ZeRO owned-shard layout (``bucket_shard``)."""
         if self.zero:
             self.zero_sync_state()
         self.side_sync()
@@ -364,27 +395,45 @@ class FFNTrainer:
             loc = self._local_from_full(p)
             for name in ("w2", "w1"):
                 src = loc[name]
+                e = self.entry[(l, name)]
+                if self.zero:
+                    srcf = src.to(device=target.device, dtype=torch.float32).reshape(-1)
+                    for a, b, go in self._owned_segments(e.offset, e.offset + e.numel):
+                        target[go:go + (b - a)].copy_(srcf[a - e.offset:b - e.offset])
+                    if target is self.master:
+                        self._view(self.copy, e).copy_(srcf.view(e.shape))  # RNE cast, as cast_
+                    continue
                 if self.fsdp:
                     rows = src.shape[0] // d
                     src = src[dr * rows:(dr + 1) * rows]
-                self._view(target, self.entry[(l, name)]).copy_(src.to(torch.float32))
-        if target is self.master and not self.shared_copy:
+                self._view(target, e).copy_(src.to(torch.float32))
+        if target is self.master and not self.shared_copy and not self.zero:
             cast_(self.master, self.copy)
 
     @torch.no_grad()
+    def refresh_copy(self) -> None:
+        """Recompute the compute-dtype working copy from the fp32 master after the master was written
+        directly (checkpoint load).  ZeRO: every rank casts its shard and all-gathers (collective)."""
+        if self.shared_copy:
+            return
+        if not self.zero:
+            cast_(self.master, self.copy)
+            return
+        grp = self.mesh.group("dp_ag")
+        for b, (s_, e_, _) in enumerate(self.buckets):
+            ss, se, go = self.bucket_shard[b]
+            self.copy[ss:se].copy_(self.master[go:go + (se - ss)])
+            src = self.copy[ss:se].clone() if self.device.type != "cuda" else self.copy[ss:se]
+            comm.all_gather_into(self.copy[s_:e_], src, grp, async_op=False)
+
+    @torch.no_grad()
     def zero_sync_state(self) -> None:
-        """ZeRO: finish in-flight parameter all-gathers and all-gather the fp32 master (and Adam moment)
-        shards so the flat buffers hold full values on every rank (checkpoint / gather).  Collective."""
+        """ZeRO: make the current stream wait for every in-flight parameter all-gather (checkpoint, readout,
+        teardown).  The fp32 state stays sharded; ``full_flat`` gathers a full copy when one is needed."""
         if not self.zero:
             return
         for b in range(len(self.buckets)):
             self._zero_wait_ag(b)
-        bufs = [self.master] + ([self.adam_m, self.adam_v] if self.cfg.optimizer == "adam" else [])
-        grp = self.mesh.group("dp_ag")
-        for buf in bufs:
-            for b, (s_, e_, _) in enumerate(self.buckets):
-                ss, se, _ = self.bucket_shard[b]
-                comm.all_gather_into(buf[s_:e_], buf[ss:se].clone(), grp, async_op=False)
 
     @torch.no_grad()
     def local_params(self, flat: torch.Tensor | None = None) -> list[dict]:
@@ -393,6 +442,9 @@ class FFNTrainer:
         self.side_sync()
         self.ddp_sync()
         src = self.master if flat is None else flat
+        if self.zero:
+            self.zero_sync_state()
+            src = self.full_flat(src)
         out = []
         for l in range(self.L):
             p = {}
@@ -412,8 +464,6 @@ class FFNTrainer:
     @torch.no_grad()
     def gather_full_params(self, flat: torch.Tensor | None = None) -> list[dict] | None:
         """Full logical fp32 tensors on CPU at global rank 0 (None elsewhere).  Collective."""
-        if self.zero and flat is None:
-            self.zero_sync_state()
         loc = self.local_params(flat)
         res = []
         for p in loc:
@@ -501,14 +551,19 @@ class FFNTrainer:
         self.bucket_work[b] = None
         s_, e_, _ = self.buckets[b]
         ss, se, go = self.bucket_shard[b]
+        n = se - ss
         cfg = self.cfg
-        g = self.gshard[go:go + (se - ss)]
-        copy = None if self.shared_copy else self.copy[ss:se]
+        g = self.gshard[go:go + n]
+        master = self.master[go:go + n]
+        bf16_copy = self.cd == torch.bfloat16
+        copy = self.copy[ss:se] if bf16_copy else None  # bf16: written by the optimizer kernel itself
         if cfg.optimizer == "sgd":
-            sgd_step_(self.master[ss:se], g, cfg.lr, copy=copy)
+            sgd_step_(master, g, cfg.lr, copy=copy)
         else:
-            adam_step_(self.master[ss:se], g, self.adam_m[ss:se], self.adam_v[ss:se], self.step_count, cfg.lr,
+            adam_step_(master, g, self.adam_m[go:go + n], self.adam_v[go:go + n], self.step_count, cfg.lr,
                        cfg.adam_b1, cfg.adam_b2, cfg.adam_eps, cfg.weight_decay, copy=copy)
+        if not bf16_copy:
+            self.copy[ss:se].copy_(master)  # fp32 compute: the working copy is a separate full buffer
         src = self.copy[ss:se]
         if self.device.type != "cuda":
             src = src.clone()  # gloo: keep input and output of the all-gather disjoint

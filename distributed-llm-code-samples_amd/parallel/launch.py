@@ -60,7 +60,7 @@ def draw_seeds(cfg: TrainConfig, seed: int) -> torch.Tensor:
 def run_rank(rank: int, world: int, cfg_dict: dict, method: int, backend: str, port: int, opts: dict,
              queue=None) -> dict | None:
     """Body of one rank: init comm, build mesh + engine, train, report.  Returns rank 0's record."""
-    from ..utils.checkpoint import load_checkpoint, save_checkpoint
+    from ..utils.checkpoint import load_into, save_checkpoint
     from ..utils.profiling import maybe_profile
     from .engine import FFNTrainer
     from .mesh import Mesh, init_distributed
@@ -88,9 +88,10 @@ def run_rank(rank: int, world: int, cfg_dict: dict, method: int, backend: str, p
     seeds = torch.as_tensor(opts["seeds"], dtype=torch.int64) if opts.get("seeds") is not None \
         else draw_seeds(cfg, seed)
     my_seeds = stripe_seeds(seeds, dp, mesh.dp_rank) if dp > 1 else seeds
-    start_step = 0
+    start_step, ckpt_read = 0, 0
     if opts.get("resume"):
-        start_step = load_checkpoint(eng, opts["resume"])
+        meta, ckpt_read = load_into(eng, opts["resume"])
+        start_step = int(meta["step"])
     data = make_data(cfg.data, cfg.tokens, cfg.model.D, cfg.torch_dtype, device)
     timer = StepTimer(device)
     stop_after = int(opts.get("stop_after") or len(my_seeds))
@@ -125,6 +126,13 @@ def run_rank(rank: int, world: int, cfg_dict: dict, method: int, backend: str, p
         save_checkpoint(eng, opts["ckpt_dir"], step=done, fmt=opts.get("ckpt_format", "consolidated"),
                         meta={"method": method, "seed": seed, "cfg": cfg_dict})
     full = eng.gather_full_params() if opts.get("return_params", True) else None
+    read_max = ckpt_read
+    if world > 1 or opts.get("force_dist"):
+        import torch.distributed as dist
+
+        t = torch.tensor([ckpt_read], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        read_max = int(t.item())
     rec = None
     if rank == 0:
         steps = done - start_step
@@ -137,6 +145,11 @@ def run_rank(rank: int, world: int, cfg_dict: dict, method: int, backend: str, p
             "slices": [(p["w1"][:5, :5].clone(), p["w2"][:5, :5].clone()) for p in full] if full else None,
             "params": full if opts.get("return_full", False) else None,
             "peak_hbm_gib": torch.cuda.max_memory_allocated(device) / 2**30 if device.type == "cuda" else 0.0,
+            # per-rank persistent state (elements): ZeRO keeps 1/dp of the fp32 master / moments
+            "state_numel": {"master": eng.master.numel(), "total": eng.total, "copy": eng.copy.numel(),
+                            "grads": eng.grads.numel(),
+                            "adam": eng.adam_m.numel() if getattr(eng, "adam_m", None) is not None else 0},
+            "ckpt_bytes_read_max": read_max,
         }
     if world > 1 or opts.get("force_dist"):
         import torch.distributed as dist

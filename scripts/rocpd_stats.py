@@ -19,6 +19,9 @@ def main():
     ap.add_argument("db")
     ap.add_argument("--last_ms", type=float, default=0.0)
     ap.add_argument("--top", type=int, default=25)
+    ap.add_argument("--step_marker", default="",
+                    help="substring of the kernel that starts a step (e.g. 'rng_normal_kernel<unsigned short>'): "
+                         "print the timeline of the second-to-last complete step instead of --last_ms")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     rows = c.execute("select name, start, end, grid_x, workgroup_x from kernels order by start").fetchall()
@@ -31,12 +34,20 @@ def main():
     for n, (k, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:a.top]:
         print(f"{short(n):88s} {k:6d} {t / k / 1e3:9.1f} {t / 1e6:9.2f} {100 * t / tot:6.2f}")
     print(f"total kernel time {tot / 1e6:.2f} ms over {len(rows)} dispatches")
-    if a.last_ms > 0 and rows:
+    win = []
+    if a.step_marker and rows:
+        starts = [i for i, r in enumerate(rows) if a.step_marker in r[0]]
+        # the marker may occur several times per step (x and dy draws): steps start at every other one
+        if len(starts) >= 6:
+            i0, i1 = starts[-6], starts[-4]
+            win = rows[i0:i1]
+    elif a.last_ms > 0 and rows:
         t1 = max(r[2] for r in rows)
         cut = t1 - a.last_ms * 1e6
         win = [r for r in rows if r[1] >= cut]
+    if win:
         busy, last = 0, 0
-        print(f"\nlast {a.last_ms} ms window: {len(win)} dispatches")
+        print(f"\nwindow: {len(win)} dispatches")
         for n, s, e, gx, wx in win:
             gap = (s - last) / 1e3 if last else 0.0
             print(f"  +{(s - win[0][1]) / 1e3:9.1f} us  {(e - s) / 1e3:8.1f} us  gap {gap:7.1f}  grid {gx // max(wx, 1):6d}  {short(n, 70)}")
