@@ -110,7 +110,8 @@ def layer_fwd(x: torch.Tensor, w1: torch.Tensor, w2: torch.Tensor, act: str, gat
 
 def layer_bwd(dy: torch.Tensor, x: torch.Tensor, w1: torch.Tensor, w2: torch.Tensor, act: str, gated: bool,
               a: torch.Tensor, h: torch.Tensor | None, gw1, gw2, da_buf: torch.Tensor,
-              dx_out: torch.Tensor | None, hooks=None, mask: torch.Tensor | None = None) -> torch.Tensor | None:
+              dx_out: torch.Tensor | None, hooks=None, mask: torch.Tensor | None = None,
+              dx_first: bool = False) -> torch.Tensor | None:
     """Backward of one layer; returns dx.
 
     ``gw1``/``gw2`` are either gradient tensors (overwritten) or dicts of ``gemm`` keyword arguments for the
@@ -119,8 +120,10 @@ def layer_bwd(dy: torch.Tensor, x: torch.Tensor, w1: torch.Tensor, w2: torch.Ten
 
     Order ``da, dW2, dx, dW1``: every dgrad that reads a weight runs before that weight's (possibly fused)
     update, a TP all-reduce of ``dx`` overlaps the dW1 GEMM, and ``hooks`` (``after_w2``, ``after_dx``,
-    ``after_w1``) mark the points where gradient collectives can be issued.  Without ``dx`` (layer 0)
-    the order is ``da, dW1, dW2`` (the engine's flat layout follows the completion order).
+    ``after_w1``) mark the points where gradient collectives can be issued.  ``dx_first`` (tensor parallel):
+    ``da, dx, dW2, dW1`` -- the input-gradient all-reduce, on which the next layer's whole backward waits,
+    then overlaps BOTH weight-gradient GEMMs.  Without ``dx`` (layer 0) the order is ``da, dW1, dW2`` (the
+    engine's flat layout follows the completion order).
     """
     if gated:
         gemm(dy, w2, "nn", out=da_buf, epi="dglu", act=act, aux=h)    # [dg|du] interleaved [T, 2F]
@@ -138,11 +141,14 @@ def layer_bwd(dy: torch.Tensor, x: torch.Tensor, w1: torch.Tensor, w2: torch.Ten
         if hooks is not None:
             hooks.after_w2()
         return None
+    if dx_first:
+        dx = gemm(da_buf, w1, "nn", out=dx_out)                       # dx = da·W1         [T, D]
+        if hooks is not None:
+            hooks.after_dx(dx)
     gemm(dy, a, "tn", **kw2)                                          # dW2 = dyᵀ·a        [D, F]
     if hooks is not None:
         hooks.after_w2()
-    dx = None
-    if dx_out is not None:
+    if not dx_first:
         dx = gemm(da_buf, w1, "nn", out=dx_out)                       # dx = da·W1         [T, D]
         if hooks is not None:
             hooks.after_dx(dx)

@@ -235,6 +235,19 @@ class FFNTrainer:
             if relu_mask_supported(T, self.F_loc, D, self.cd):
                 self.masks = [torch.empty(relu_mask_bytes(T, self.F_loc), dtype=torch.uint8, device=dev)
                               for _ in range(nA)]
+        # TP forward row chunks (see TrainConfig.tp_chunks): whole 256-row tiles per chunk; the ReLU bitmask is
+        # written per chunk (tile-native layout, tile rows contiguous), so chunk GEMMs must stay on its kernels
+        self.tp_chunks = 1
+        c = max(1, cfg.tp_chunks)
+        if t > 1 and not self.sp and c > 1 and T % (256 * c) == 0:
+            if self.masks is None:
+                self.tp_chunks = c
+            else:
+                from ..ops.gemm import relu_mask_supported
+
+                if relu_mask_supported(T // c, self.F_loc, D, self.cd):
+                    self.tp_chunks = c
+        self._tp_pending = None
         # concurrent weight-gradient stream (single device, fused optimizer, kept activations): the dgrad
         # chain (da, dx) stays on the compute stream, dW2 / dW1 run on a side stream after the dgrad that
         # last reads the weight they update; da / dx buffers rotate so the side stream's reads never race
@@ -690,12 +703,19 @@ class FFNTrainer:
                 elif self.ddp:
                     def before2(l=l):
                         self._ddp_wait(l, "w2")
+                if self.tp_chunks > 1:
+                    self._tp_fwd_chunked(l, w1, w2, a, h, before2)
+                    continue
                 layer_fwd(self.xs[l], w1, w2, act, gated, a, h, self.xs[l + 1], before_fwd2=before2,
                           mask=self._mask(l))
                 if self.tp_car is not None:
                     self.tp_car.all_reduce(self.xs[l + 1])
                 elif self.mesh.tp > 1:
                     comm.all_reduce(self.xs[l + 1], tpg, async_op=True).wait()
+        if self._tp_pending is not None:
+            for w in self._tp_pending:
+                w.wait()
+            self._tp_pending = None
         y = self.xs[L]
 
         self._unmark(mark)
@@ -741,18 +761,20 @@ class FFNTrainer:
                     recompute_fwd1(xin, w1, act, gated, a, h, mask=self._mask(l))
                 hooks_sp = _SPHooks(self, l)
                 dxp = layer_bwd(self.dyfull, xin, w1, w2, act, gated, a, h, gw1, gw2, self.da,
-                                self.dxb[l % 2] if need_dx else None, hooks_sp, mask=self._mask(l))
+                                self.dxb[l % 2] if need_dx else None, hooks_sp, mask=self._mask(l),
+                                dx_first=cfg.tp_overlap)
                 if dxp is not None:
-                    out = self.dxs[l % 2]
-                    comm.reduce_scatter_into(out, dxp, tpg, async_op=True).wait()
-                    g = out
+                    if hooks_sp.rs_work is not None:
+                        hooks_sp.rs_work.wait()
+                    g = self.dxs[l % 2]
             elif self.wg_stream is not None:
                 g = self._layer_bwd_concurrent(l, g, w1, w2, a, h, gw1, gw2, need_dx)
             else:
                 if not keep:
                     recompute_fwd1(self.xs[l], w1, act, gated, a, h, mask=self._mask(l))
                 dx = layer_bwd(g, self.xs[l], w1, w2, act, gated, a, h, gw1, gw2, self.da,
-                               self.dxb[l % 2] if need_dx else None, hooks, mask=self._mask(l))
+                               self.dxb[l % 2] if need_dx else None, hooks, mask=self._mask(l),
+                               dx_first=self.mesh.tp > 1 and cfg.tp_overlap)
                 if dx is not None:
                     g = dx
             if self.zero:
@@ -798,6 +820,30 @@ class FFNTrainer:
             self.check_health()
         return y
 
+    def _tp_fwd_chunked(self, l: int, w1, w2, a, h, before2) -> None:
+        """Tensor-parallel forward of layer l in ``tp_chunks`` row chunks: chunk i's partial-output all-reduce
+        is issued as soon as its two GEMMs are done and runs while chunk i+1 computes; the next layer's chunk i
+        waits (stream wait, no host block) only for that chunk's all-reduce.  Rows are independent in the FFN,
+        so the results equal the one-all-reduce-per-layer schedule (reference: sync all_reduce(y),
+        train_ffns.py:300-303)."""
+        c, x, y = self.tp_chunks, self.xs[l], self.xs[l + 1]
+        rows = self.T // c
+        mask = self._mask(l)
+        mband = (rows // 256) * (self.F_loc // 256) * 8192 if mask is not None else 0  # mask bytes per chunk
+        prev, works = self._tp_pending, []
+        for ci in range(c):
+            r = slice(ci * rows, (ci + 1) * rows)
+            if prev is not None:
+                prev[ci].wait()
+            layer_fwd(x[r], w1, w2, self.act, self.gated, a[r], h[r] if h is not None else None, y[r],
+                      before_fwd2=before2 if ci == 0 else None,
+                      mask=mask[ci * mband:(ci + 1) * mband] if mask is not None else None)
+            if self.tp_car is not None:
+                works.append(self.tp_car.all_reduce_async(y[r]))
+            else:
+                works.append(comm.all_reduce(y[r], self.mesh.group("tp"), async_op=True))
+        self._tp_pending = works
+
     def check_health(self) -> None:
         """Raise if an asynchronous failure was recorded on the device: a timed-out barrier of the custom
         TP all-reduce (whose results are then NaN-poisoned, csrc/car.hip).  Synchronises the device; called
@@ -841,7 +887,17 @@ class FFNTrainer:
 
 
 class _SPHooks(_Hooks):
-    """Sequence-parallel variant: the dx reduce-scatter is issued by the caller after the layer."""
+    """Sequence-parallel variant: the partial dx is reduce-scattered over T (asynchronously, overlapping the
+    weight-gradient GEMMs that follow it in the ``dx_first`` order); the caller waits after the layer."""
+
+    rs_work = None
 
     def after_dx(self, dx):
-        return None
+        e = self.eng
+        self.rs_work = comm.reduce_scatter_into(e.dxs[self.layer % 2], dx, e.mesh.group("tp"), async_op=True)
+        if not e.cfg.tp_overlap:
+            self.rs_work.wait()
+            self.rs_work = None
+
+    def after_w1(self):
+        self.eng._grad_ready(self.layer, "w1")

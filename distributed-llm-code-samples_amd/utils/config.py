@@ -63,7 +63,10 @@ class TrainConfig:
     data: str = "device"             # device (Philox on GPU) | cpu_compat (reference CPU generator)
     skip_input_grad: bool = True     # layer-0 dx is never consumed (reference computes it, :68)
     separate_streams: bool = True    # one communicator/stream per comm role
-    tp_overlap: bool = True          # overlap the TP dx all-reduce with the dW1 GEMM
+    tp_overlap: bool = True          # overlap the TP dx all-reduce with the dW2 / dW1 GEMMs
+    tp_chunks: int = 4               # TP forward: split T into this many row chunks; chunk i's y all-reduce
+                                     # runs while chunk i+1 computes, and the next layer's chunk i starts as
+                                     # soon as that one all-reduce is done (1 = one all-reduce per layer)
     relu_mask: bool = True           # ReLU: the dgrad reads a 1-bit activation mask written by the forward
                                      # GEMM instead of the bf16 activation (GPU, 8-phase kernel shapes)
     wgrad_stream: bool = False       # single device, fused optimizer: weight-gradient GEMMs on a second

@@ -223,3 +223,17 @@ def test_sharded_zero_resume_continues_training(tmp_path, free_port):
     a = _run(cfg, 3, 2, free_port + 2, resume=ck_sh)
     b = _run(cfg, 3, 2, free_port + 3, resume=ck_co)
     _close(a, b, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("chunks", [1, 4])
+def test_tp_chunked_forward_pipeline(chunks, free_port):
+    """TP forward in row chunks (each chunk's y all-reduce overlapping the next chunk's GEMMs, the next
+    layer's chunk waiting only for its own all-reduce) and the dx-first backward (dx all-reduce overlapping
+    both weight-gradient GEMMs) train exactly like the single device (train_ffns.py:290-312)."""
+    cfg = _cfg(D=32, F=64, L=3, T=1024, steps=2, tp_chunks=chunks)
+    _close(_run(cfg, 4, 2, free_port), _oracle(cfg, 1))
+
+
+def test_sequence_parallel_async_dx(free_port):
+    cfg = _cfg(D=32, F=64, L=3, T=64, steps=2, sequence_parallel=True)
+    _close(_run(cfg, 4, 2, free_port), _oracle(cfg, 1))
