@@ -111,8 +111,6 @@ def parse(argv=None):
                    help="bf16 GEMM main-loop schedule (auto = 8-phase staggered when K % 128 == 0)")
     p.add_argument("--tpb", type=int, default=0,
                    help="tiles per persistent 8-phase GEMM block (0 = auto: 2, or 1 for gated stacks; 1 = off)")
-    p.add_argument("--skew", type=int, default=-1,
-                   help="epilogue-skew groups of the persistent GEMMs (-1 = library default, <= 1 off)")
     p.add_argument("--wgrad_stream", action="store_true",
                    help="N=1: weight-gradient GEMMs (fused SGD) on a second stream, concurrent with the dgrads")
     p.add_argument("--no_relu_mask", action="store_true",
@@ -284,10 +282,6 @@ def main(argv=None) -> int:
         from dllm.ops.gemm import set_bf16_variant
 
         set_bf16_variant(a.gemm_variant)
-    if a.skew >= 0 and not cpu:
-        from dllm.ops.gemm import set_epilogue_skew
-
-        set_epilogue_skew(a.skew)
     ffn = a.ffn_dim or (a.mp_ffn_dim if a.method == "tp" else 0)
     model = ModelConfig(model_size=a.model_size, ffn_dim=ffn, layers=a.layers, act=a.act, gated=a.gated)
     head = run_method(a, a.method, n, world, dev, a.steps, a.warmup, a.force_comm, model,

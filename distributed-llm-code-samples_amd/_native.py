@@ -26,7 +26,7 @@ _SIGS = {
     "dllm_gemm": (c_int, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_long, c_void_p, c_long, c_void_p, c_long,
                           c_void_p, c_void_p, c_long, c_int, c_int, c_int, c_float, c_float, c_int, c_int, c_void_p,
                           c_float, c_float, c_float, c_float, c_float, c_int, c_void_p, c_void_p, c_int, c_void_p,
-                          c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
+                          c_void_p, c_int, c_int, c_int]),
     "dllm_gemm_path": (c_int, [c_int, c_int, c_int, c_int, c_int, c_long, c_long, c_long]),
     "dllm_rng_normal": (c_int, [c_void_p, c_int, c_long, c_ull, c_ull, c_float, c_void_p]),
     "dllm_rng_normal_devseed": (c_int, [c_void_p, c_int, c_long, c_void_p, c_ull, c_float, c_void_p]),

@@ -15,8 +15,7 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
               const void* B, long ldb, void* C, long ldc, const void* aux, void* aux_out, long ldaux,
               int M, int N, int K, float alpha, float beta, int group_m, int force_path, void* stream,
               float lr, float b1, float b2, float eps, float wd, int step, float* opt_m, float* opt_v,
-              int ksplit, float* workspace, void* mask, int variant, int tpb, int min_bpc, int skew,
-              float* skew_ws) {
+              int ksplit, float* workspace, void* mask, int variant, int tpb, int min_bpc) {
   if (M <= 0 || N <= 0 || K <= 0) return -1;
   if (layout < 0 || layout > 2) return -1;
   if ((epi == EPI_GLU || epi == EPI_DGLU) && (N % 32) != 0) return -1;
@@ -34,8 +33,6 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
   a.tpb_req = tpb;
   a.min_bpc = min_bpc < 1 ? 1 : min_bpc;
   a.ws = nullptr;
-  a.skew = skew;
-  a.skew_ws = skew_ws;
   // the LDS-DMA loads and 16-B / paired epilogue accesses of the MFMA paths need 16-B aligned bases
   const bool aligned_ptr = ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && ((uintptr_t)C % 16 == 0) &&
                            ((uintptr_t)aux % 16 == 0) && ((uintptr_t)aux_out % 16 == 0) &&

@@ -57,10 +57,6 @@ struct GemmArgs {
   int tpb_req;   // requested tiles per persistent block (<= 1: one block per tile)
   int min_bpc;   // minimum blocks per CU of a persistent grid (2 when collectives overlap the GEMMs)
   float* ws;     // split-K fp32 partial workspace (caller-owned, ksplit * M * N floats)
-  // epilogue skew (persistent kernels, one block per CU): blocks fall into `skew` groups whose epilogues are
-  // offset by 1/skew of a tile (see gemm_bf16_8ph); skew_ws holds one raw fp32 accumulator tile per block
-  int skew;
-  float* skew_ws;
   // ReLU activation-gradient bitmask (nullable; 8-phase kernels, bf16 out, compile-time ReLU): EPI_ACT writes
   // bit (act(h) != 0) per output element, EPI_DACT reads it instead of aux.  Tile-native layout: 8 KiB per
   // 256x256 tile (tile = tm * tiles_n + tn), 16 B per thread -- the same element->lane map in both GEMMs.
@@ -795,16 +791,7 @@ __device__ __forceinline__ GemmArgs reload_args() {
 // NPH = 8: the 8-phase schedule below (one quadrant = 16 MFMAs per wave per barrier interval).
 // NPH = 4: half-tile phases (two quadrants = 32 MFMAs per interval, two half-tiles restaged per phase):
 // halves the barrier count per MFMA (see the NPH == 4 loop).
-// SKEW (persistent only, p.skew > 1): epilogue skew.  Every persistent block runs the same number of tiles, so
-// without it all blocks reach their epilogue at the same moment and the whole chip bursts its output (and, for
-// the fused optimizer, its fp32 master read-modify-write) through HBM while no MFMA runs.  Block b belongs to
-// group g = (b / 8) % skew (spread over the XCDs); group g > 0 starts with only the first kg = g/skew of its first
-// tile's K-tiles, parks that raw fp32 accumulator in skew_ws, runs its other tiles, and finally finishes the first
-// tile from K-tile kg and adds the parked part before that tile's epilogue (two partial sums: equal to the
-// unskewed kernel up to fp32 rounding, deterministic).  The groups' epilogues are thus 1/skew of a tile apart:
-// each output burst comes from 1/skew of the chip.
-template <int LAYOUT, int EPI, typename OutT, bool STAGGER, int ACT = -1, int NPH = 8, bool PERS = false,
-          bool SKEW = false>
+template <int LAYOUT, int EPI, typename OutT, bool STAGGER, int ACT = -1, int NPH = 8, bool PERS = false>
 __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
   // slot(op, hh, buf) = ((op*2 + hh)*2 + buf) * 16 KiB: A in [0, 64K), B in [64K, 128K), so every
   // fragment read is base + a 16-bit immediate
@@ -869,57 +856,10 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
       if (q.ksplit > 1) out = (char*)q.C + (long)sp * q.M * q.ldc * sizeof(OutT);
     epilogue_256<EPI, OutT, ACT>(q, ac, tm0, tn0, wr, wc, lane, out);
   };
-  // epilogue skew: this block's group and its split point kg of the first tile (0: no split)
-  int kg = 0;
-  if constexpr (SKEW) {
-    if (pers && p.skew > 1) {
-      const int g = ((int)blockIdx.x >> 3) % (p.skew & 0xff), step = p.skew >> 8;  // step: K-tiles per group
-      kg = step > 0 ? min(2 * ((g * step + 1) / 2), nk - 2) : ((nk * g) / (p.skew & 0xff)) & ~1;
-    }
-  }
-  int item = 0;           // work item of this block (SKEW: 0 = first part of the split tile, tpb = its rest)
-  int cur_nk = kg > 0 ? kg : nk;
-  // next slot of this block (>= total: none).  SKEW state is re-derived from (item, kg) and a reloaded tpb
-  // wherever it is needed, so the main loop carries no extra live registers.
+  // next slot of this block (>= total: none)
   int next_slot = total;
-  auto begin_tile = [&]() {
-    if constexpr (SKEW) {
-      if (kg > 0) {
-        const int j = item + 1, t = reload_args().tpb;
-        next_slot = j < t ? (int)blockIdx.x + j * (int)gridDim.x : j == t ? (int)blockIdx.x : total;
-        return;
-      }
-    }
-    next_slot = pers ? slot + (int)gridDim.x : total;
-  };
-  // first K-tile of the next item (SKEW: the split tile's rest starts at kg)
-  auto next_k0 = [&]() -> int {
-    if constexpr (SKEW) return (kg > 0 && next_slot == (int)blockIdx.x) ? kg : 0;
-    return 0;
-  };
+  auto begin_tile = [&]() { next_slot = pers ? slot + (int)gridDim.x : total; };
   begin_tile();
-  // SKEW: raw accumulator tile of this block in skew_ws, [4][512 threads][8] 16-B vectors: each lane's 8
-  // consecutive vectors share one address register (immediate offsets < 4 KiB), 4 registers per tile
-  // (the per-lane address is rebuilt from an opaque thread id at each use: hoisted out of the main loop it
-  // would pin VGPRs across it)
-  auto park_base = [&]() {
-    uint32_t t = threadIdx.x;
-    asm volatile("" : "+v"(t));
-    return (f32x4_t*)(reload_args().skew_ws + (long)blockIdx.x * (BT_M * BT_N)) + t * 8;
-  };
-  auto park_acc = [&](f32x4_t (&ac)[2][2][4][2]) {
-    f32x4_t* w = park_base();
-#pragma unroll
-    for (int i = 0; i < 32; ++i) w[(i >> 3) * 4096 + (i & 7)] = ac[i >> 4][(i >> 3) & 1][(i >> 1) & 3][i & 1];
-  };
-  // the split tile's rest ran from a zero accumulator: add the parked first part before its epilogue (outside
-  // the main loop: a reload into the loop-entry accumulator made hipcc spill inside the loop)
-  auto add_parked = [&](f32x4_t (&ac)[2][2][4][2]) {
-    const f32x4_t* w = park_base();
-#pragma unroll
-    for (int i = 0; i < 32; ++i) ac[i >> 4][(i >> 3) & 1][(i >> 1) & 3][i & 1] += w[(i >> 3) * 4096 + (i & 7)];
-  };
-
 
   // stage half hh of the K-tile at `src` (K-tile base of operand op) into buffer buf
   auto stage_at = [&](int op, int hh, const uint16_t* src, int buf) {
@@ -1121,7 +1061,7 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
   }
 
   for (;;) {  // slots of this block (one pass unless persistent)
-  for (int it = 0; it < cur_nk / 2; ++it) {
+  for (int it = 0; it < nk / 2; ++it) {
 #define DLLM_PHASE_END(VMWAIT)                                      \
   if (VMWAIT) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");       \
   DLLM_LDS_WAIT();                                                   \
@@ -1129,13 +1069,12 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
     // ---- even buffer (K-tile 2it) ----
     read_a(I0{}, I0{}); read_b(I0{}, I0{}, fb0);
     stage_at(0, 1, Apf - a_kstep, 1);          // P0: A1 odd (K-tile 2it+1)
-    if (it == cur_nk / 2 - 1) {
+    if (it == nk / 2 - 1) {
       // last iteration: the remaining prefetches are the next slot's K-tiles 0/1 (or harmless re-loads)
       if (next_slot < total) {
         const GemmArgs q = reload_args();
-        const int k0 = next_k0();
-        Apf = a_base(q, next_slot) + k0 * a_kstep;
-        Bpf = b_base(q, next_slot) + k0 * b_kstep;
+        Apf = a_base(q, next_slot);
+        Bpf = b_base(q, next_slot);
       } else {
         Apf -= 2 * a_kstep;
         Bpf -= 2 * b_kstep;
@@ -1193,8 +1132,7 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
   // Apf/Bpf already point at its K-tile 2; this slot's epilogue runs meanwhile.  It touches no LDS and
   // has no barrier, so the (staggered) barrier sequence continues unchanged into the next slot's P0; its
   // memory operations are older than the next slot's P0-P3 stages and are retired by P3's counted wait.
-  if (SKEW && kg > 0 && item == 0) park_acc(acc);
-  else slot_epilogue(slot, acc);
+  slot_epilogue(slot, acc);
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -1203,9 +1141,7 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
       for (int c = 0; c < 4; ++c)
 #pragma unroll
         for (int d = 0; d < 2; ++d) acc[a][b][c][d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  if constexpr (SKEW) cur_nk = (kg > 0 && next_slot == (int)blockIdx.x) ? nk - kg : nk;
   slot = next_slot;
-  ++item;
   begin_tile();
   }  // slots
   }  // NPH == 8
@@ -1214,9 +1150,6 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
   }
   // drain the tail prefetches before the block can release its LDS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if constexpr (SKEW) {
-    if (kg > 0) add_parked(acc);  // the last item is the split tile's rest
-  }
   slot_epilogue(slot, acc);
 }
 
@@ -1520,24 +1453,10 @@ constexpr bool persistent_kernel() {
   return E == EPI_STORE || E == EPI_SGD;
 }
 
-// epilogue-skew launch: one block per CU, every block the same whole number (>= 2) of tiles
-static bool skew_grid(GemmArgs& a, int nb) {
-  const int ncu = num_cu();
-  if ((a.skew & 0xff) <= 1 || a.skew_ws == nullptr || a.min_bpc > 1 || a.ksplit != 1 || ncu <= 0 || ncu % 8) return false;
-  if (nb % ncu || nb / ncu < 2 || (a.K / BT_K) < 2 * (a.skew & 0xff)) return false;
-  a.tpb = nb / ncu;
-  return true;
-}
-
 template <int L, int E, typename OutT, int ACT, int NPH>
 static void launch_8ph_act(const GemmArgs& a0, int nb0, hipStream_t s) {
   if constexpr (NPH == 8 && persistent_kernel<L, E, OutT, ACT>()) {
     GemmArgs a = a0;
-    if (skew_grid(a, nb0)) {
-      hipLaunchKernelGGL((gemm_bf16_8ph<L, E, OutT, true, ACT, NPH, true, true>), dim3(num_cu()), dim3(512), 0, s, a);
-      return;
-    }
-    a = a0;
     const int nb = grid_8ph(a, nb0);
     if (a.tpb > 1) {
       hipLaunchKernelGGL((gemm_bf16_8ph<L, E, OutT, true, ACT, NPH, true>), dim3(nb), dim3(512), 0, s, a);

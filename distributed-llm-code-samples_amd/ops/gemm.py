@@ -163,30 +163,19 @@ _VARIANT = {"name": "auto"}
 # Launch policy of the 256x256 bf16 kernels (tiles per persistent block, minimum blocks per CU): Python-level
 # defaults that every call passes to the library explicitly -- the native side keeps no mutable state, so
 # GEMMs issued concurrently on different streams never race on a setting.
-_POLICY = {"tpb": 2, "min_bpc": 1, "skew": 4}
-SKEW_TILE_FLOATS = 256 * 256  # one parked fp32 accumulator tile per persistent block
+_POLICY = {"tpb": 2, "min_bpc": 1}
 # split-K fp32 partial workspaces, cached per (device, stream): a GEMM only ever reuses its own stream's
 # buffer, so stream order serialises the reuse
 _WS: dict = {}
 
 
-def _splitk_workspace(numel: int, device: torch.device, kind: str = "splitk") -> torch.Tensor:
-    key = (kind, device.index, torch.cuda.current_stream(device).cuda_stream)
+def _splitk_workspace(numel: int, device: torch.device) -> torch.Tensor:
+    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
     ws = _WS.get(key)
     if ws is None or ws.numel() < numel:
         ws = torch.empty(numel, dtype=torch.float32, device=device)
         _WS[key] = ws
     return ws
-
-
-_NUM_CU: dict = {}
-
-
-def _num_cu(device: torch.device) -> int:
-    n = _NUM_CU.get(device.index)
-    if n is None:
-        n = _NUM_CU[device.index] = torch.cuda.get_device_properties(device).multi_processor_count
-    return n
 
 
 def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None = None, *, epi: str = "store",
@@ -241,11 +230,6 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
             ws = _splitk_workspace(ksplit * M * N, a.device)
         else:
             ksplit = 1
-    skew, skew_ws = 0, None
-    if ((_POLICY["skew"] & 0xff) > 1 and _POLICY["min_bpc"] == 1 and ksplit == 1 and a.dtype == torch.bfloat16
-            and force in (None, "mfma_bf16") and (M // 256) * (N // 256) >= 2 * _num_cu(a.device)):
-        skew = _POLICY["skew"]
-        skew_ws = _splitk_workspace(_num_cu(a.device) * SKEW_TILE_FLOATS, a.device, "skew")
     obs = _observe.active()
     if obs is not None:
         obs.gemm_begin()
@@ -260,8 +244,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
                      opt_v.data_ptr() if opt_v is not None else None, ksplit,
                      ws.data_ptr() if ws is not None else None,
                      _mask_ptr(mask, M, N) if mask is not None else None,
-                     BF16_VARIANTS[_VARIANT["name"]], _POLICY["tpb"], _POLICY["min_bpc"], skew,
-                     skew_ws.data_ptr() if skew_ws is not None else None)
+                     BF16_VARIANTS[_VARIANT["name"]], _POLICY["tpb"], _POLICY["min_bpc"])
     _native.check(rc, f"dllm_gemm({layout},{epi},M={M},N={N},K={K})")
     if obs is not None:
         obs.gemm_end()
@@ -305,17 +288,6 @@ def set_tiles_per_block(n: int) -> int:
     Default 2.  Returns the previous setting."""
     old = _POLICY["tpb"]
     _POLICY["tpb"] = max(1, int(n))
-    return old
-
-
-def set_epilogue_skew(groups: int) -> int:
-    """Epilogue skew of the persistent GEMMs (default 4 groups; <= 1 off): with one block per CU and every block
-    running the same number of tiles, blocks fall into ``groups`` groups whose epilogues are 1/groups of a tile
-    apart, so each output burst (and the fused optimizer's fp32 read-modify-write) comes from 1/groups of the
-    chip while the rest keeps its MFMAs busy.  Bitwise identical results.  Only with one block per CU (not while
-    collectives overlap the GEMMs: ``set_min_blocks_per_cu(2)``).  Returns the previous setting."""
-    old = _POLICY["skew"]
-    _POLICY["skew"] = max(0, int(groups))
     return old
 
 

@@ -317,54 +317,6 @@ def test_persistent_blocks_bitwise_equal(tpb, layout, epi):
         assert torch.equal(x, y)
 
 
-@pytest.mark.parametrize("layout,epi", [("nt", "act"), ("nt", "store"), ("nn", "dact"), ("nn", "store"),
-                                        ("tn", "sgd"), ("tn", "store_f32")])
-def test_epilogue_skew_matches_unskewed(layout, epi):
-    """Epilogue skew (one persistent block per CU, groups offset by 1/4 tile, the first tile's partial sum
-    parked and added back) == the unskewed persistent kernel up to fp32 rounding of that one split, is
-    deterministic run to run, and matches the fp64 reference."""
-    from dllm.ops.gemm import relu_mask_bytes, set_epilogue_skew
-
-    M, N, K = 4096, 8192, 1024  # 512 tiles = 2 per CU on 256 CUs, 16 K-tiles: split points 4 / 8 / 12
-    a, b = _operands(layout, M, N, K, torch.bfloat16, seed=47)
-    a, b = a.cuda(), b.cuda()
-    runs = []
-    for sk in (0, 4, 4):
-        old = set_epilogue_skew(sk)
-        try:
-            kw = {}
-            if epi in ("act", "store", "dact"):
-                out = torch.zeros(M, N, dtype=torch.bfloat16, device="cuda")
-                if epi == "act":
-                    kw = dict(epi="act", act="relu",
-                              mask=torch.zeros(relu_mask_bytes(M, N), dtype=torch.uint8, device="cuda"))
-                elif epi == "dact":
-                    kw = dict(epi="dact", act="relu", aux=_mk((M, N), torch.bfloat16, 5).cuda())
-            elif epi == "store_f32":
-                out = torch.zeros(M, N, dtype=torch.float32, device="cuda")
-            else:
-                out = _mk((M, N), torch.float32, 9).cuda()
-                kw = dict(epi="sgd", lr=1e-3, aux_out=torch.zeros(M, N, dtype=torch.bfloat16, device="cuda"))
-            gemm(a, b, layout, out=out, **kw)
-            torch.cuda.synchronize()
-            runs.append([out] + [v for v in kw.values() if isinstance(v, torch.Tensor)])
-        finally:
-            set_epilogue_skew(old)
-    for x, y in zip(runs[1], runs[2]):
-        assert torch.equal(x, y)  # deterministic
-    plain, skew = runs[0][0], runs[1][0]
-    if plain.dtype == torch.bfloat16:
-        ulp = (plain.float() - skew.float()).abs() <= plain.float().abs() * 2 ** -7 + 1e-30
-        assert ulp.all() and (plain != skew).float().mean() < 0.05
-    else:
-        torch.testing.assert_close(skew, plain, rtol=1e-5, atol=1e-6)
-    if epi == "store_f32":
-        ref = _ref(a.cpu(), b.cpu(), layout)
-        assert ((skew.cpu().double() - ref).abs().max() / ref.abs().max()) < 1e-5
-    if epi == "act":  # the ReLU bitmask is written by the split tile's final epilogue too
-        assert torch.equal(runs[0][1], runs[1][1]) or (runs[0][1] != runs[1][1]).float().mean() < 1e-3
-
-
 @pytest.mark.parametrize("layout", ["nt", "tn"])
 def test_persistent_blocks_splitk_bitwise_equal(layout):
     """Persistent blocks over split-K slices (slot = tile x slice) == one block per slice, bitwise."""
