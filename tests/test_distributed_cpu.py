@@ -237,3 +237,30 @@ def test_tp_chunked_forward_pipeline(chunks, free_port):
 def test_sequence_parallel_async_dx(free_port):
     cfg = _cfg(D=32, F=64, L=3, T=64, steps=2, sequence_parallel=True)
     _close(_run(cfg, 4, 2, free_port), _oracle(cfg, 1))
+
+
+def _update_err(got, want, init) -> float:
+    worst = 0.0
+    for g, w, i in zip(got, want, init):
+        for k in w:
+            dg, dw = g[k].double() - i[k].double(), w[k].double() - i[k].double()
+            worst = max(worst, float((dg - dw).norm() / dw.norm()))
+    return worst
+
+
+@pytest.mark.parametrize("method", [2, 6])
+def test_bf16_gradient_collectives_vs_fp32_oracle(method, free_port):
+    """bf16 compute with bf16 gradient buckets all-reduced (DDP) / reduce-scattered (ZeRO-2) over 2 ranks --
+    the bench's N>1 default -- pinned against (a) the same bf16-compute run with fp32 gradient collectives
+    and (b) the fp32 reference algorithm (train_ffns.py:144-172, fp32 everywhere, summed gradients).
+    Measured on this config (relative error of each weight's UPDATE, trained - init): bf16 instead of fp32
+    gradient buckets moves the update by 2.5 % (a); bf16 COMPUTE is 6.6-6.8 % from the fp32 oracle (b) with
+    either gradient dtype -- a single device gives the same -- because at D=64, T=64 the bf16 rounding of h
+    near 0 flips ReLU masks, which the second step then amplifies.  Tolerances: (a) 5e-2, (b) 0.1."""
+    cfg = _cfg(D=64, F=256, L=2, T=64, steps=4, dtype="bf16", grad_dtype="bf16")
+    cfg32 = _cfg(D=64, F=256, L=2, T=64, steps=4, dtype="bf16", grad_dtype="fp32")
+    got = _run(cfg, method, 2, free_port)
+    ref_grads32 = _run(cfg32, method, 2, free_port + 1)
+    init = build_params(cfg, "cpu_compat", SEED, "cpu")
+    assert _update_err(got, ref_grads32, init) < 5e-2
+    assert _update_err(got, _oracle(cfg, 2), init) < 0.1
