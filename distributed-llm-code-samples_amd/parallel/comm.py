@@ -118,6 +118,40 @@ def reduce_scatter_into(out: torch.Tensor, full: torch.Tensor, group, async_op: 
     return _finish(w, async_op) if (async_op or _SERIALIZE) else (w.wait(), Done())[1]
 
 
+class _Many:
+    """Completion of several collectives issued together."""
+
+    def __init__(self, works):
+        self.works = works
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+        return True
+
+    def is_completed(self):
+        return all(w.is_completed() for w in self.works)
+
+
+def all_gather_into_many(pairs, group, async_op: bool = True):
+    """All-gathers ``(out, shard)`` issued as ONE group: the native layer fuses them with
+    ncclGroupStart/End (one launch, one completion event); torch / gloo issue them back to back."""
+    if group is not None and _native(group) and not _SERIALIZE:
+        w = _issue(group, lambda: group.all_gather_into_many([(o.view(-1), sh.reshape(-1)) for o, sh in pairs]))
+        return w if async_op else (w.wait(), Done())[1]
+    w = _Many([all_gather_into(o, sh, group, async_op=True) for o, sh in pairs])
+    return w if async_op else (w.wait(), Done())[1]
+
+
+def reduce_scatter_into_many(pairs, group, async_op: bool = True):
+    """Reduce-scatters ``(out, full)`` issued as ONE group (see ``all_gather_into_many``)."""
+    if group is not None and _native(group) and not _SERIALIZE:
+        w = _issue(group, lambda: group.reduce_scatter_into_many([(o.view(-1), f.reshape(-1)) for o, f in pairs]))
+        return w if async_op else (w.wait(), Done())[1]
+    w = _Many([reduce_scatter_into(o, f, group, async_op=True) for o, f in pairs])
+    return w if async_op else (w.wait(), Done())[1]
+
+
 def gather_to_rank0(t: torch.Tensor, group=None) -> list[torch.Tensor] | None:
     """Gather equally-shaped tensors from every rank of ``group`` onto rank 0 of that group (CPU copies)."""
     if group is not None and _native(group):

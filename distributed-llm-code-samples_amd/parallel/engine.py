@@ -548,8 +548,9 @@ class FFNTrainer:
         elif self.fsdp and name == self.layer_order(l)[1]:
             slot = l % 2
             g = self.gring[slot]
-            works = [comm.reduce_scatter_into(self.grad_view(l, n), g[n], self.mesh.group("dp_rs"), async_op=True)
-                     for n in ("w2", "w1")]
+            # the layer's two gradient reduce-scatters as one group (native: one fused RCCL launch)
+            works = [comm.reduce_scatter_into_many([(self.grad_view(l, n), g[n]) for n in ("w2", "w1")],
+                                                   self.mesh.group("dp_rs"), async_op=True)]
             self.rs_pending[slot] = (l, works)
 
     def _zero_finish(self, b: int, side: bool = False) -> None:
@@ -625,8 +626,9 @@ class FFNTrainer:
     def _fsdp_gather(self, l: int) -> None:
         slot = l % 2
         grp = self.mesh.group("dp_ag")
-        self.ag_work[slot] = [comm.all_gather_into(self.wring[slot][n], self.copy_view(l, n), grp, async_op=True)
-                              for n in ("w2", "w1")]
+        # the layer's W2 and W1 shard all-gathers as one group (native: one fused RCCL launch)
+        self.ag_work[slot] = [comm.all_gather_into_many([(self.wring[slot][n], self.copy_view(l, n))
+                                                         for n in ("w2", "w1")], grp, async_op=True)]
         self.ag_layer[slot] = l
 
     def _fsdp_weights(self, l: int) -> tuple[torch.Tensor, torch.Tensor]:

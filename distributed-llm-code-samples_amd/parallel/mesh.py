@@ -62,6 +62,7 @@ class Mesh:
     groups: dict = field(default_factory=dict)
     dp_ranks: list = field(default_factory=list)
     tp_ranks: list = field(default_factory=list)
+    native_world: object = None  # native backend: the communicator the role communicators are split from
 
     @property
     def world(self) -> int:
@@ -98,6 +99,12 @@ class Mesh:
                 else:
                     g.destroy()
         self.groups.clear()
+        if self.native_world is not None:
+            if abort:
+                self.native_world.abort()
+            else:
+                self.native_world.destroy()
+            self.native_world = None
 
     @classmethod
     def build(cls, dp: int, tp: int, separate_streams: bool = True, force: bool = False,
@@ -116,9 +123,16 @@ class Mesh:
         if not dist.is_initialized() or (world == 1 and not force):
             return m
         if comm_backend == "native":
-            from .rccl import new_role_group
+            # one job-wide RCCL communicator (store-bootstrapped uniqueId), then every role communicator is
+            # ncclCommSplit from it: color = this rank's dp group (dp roles) or tp group (tp role), key = its
+            # position in that group -- the 2-D mesh is carved out of one bootstrap
+            from .rccl import NativeGroup, new_world_group
 
             dev = device or torch.device("cuda", torch.cuda.current_device())
+            world_comm = new_world_group(dev)
+            m.native_world = world_comm
+            dp_groups = [[d * tp + t for d in range(dp)] for t in range(tp)]
+            tp_groups = [[d * tp + t for t in range(tp)] for d in range(dp)]
             for role in ROLES:
                 axis = dp if role.startswith("dp") else tp
                 if axis == 1 and not force:
@@ -126,8 +140,7 @@ class Mesh:
                 if not separate_streams and role in ("dp_ag", "dp_rs") and "dp_ar" in m.groups:
                     m.groups[role] = m.groups["dp_ar"]
                     continue
-                ranks = m.tp_ranks if role == "tp" else m.dp_ranks
-                m.groups[role] = new_role_group(ranks, role, dev)
+                m.groups[role] = NativeGroup.split(world_comm, tp_groups if role == "tp" else dp_groups, dev)
             return m
         # every rank creates every group in the same order (new_group is collective)
         for role in ROLES:

@@ -97,34 +97,58 @@ class NativeWork:
         _check(_lib().dllm_event_synchronize(self.ev.h), "hipEventSynchronize")
 
 
+NCCL_SPLIT_NOCOLOR = -1
+
+
 class NativeGroup:
     """One RCCL communicator over ``ranks`` (global ranks) with its own stream.  Collective over the
-    members only (non-members do not participate), bootstrapped through the default store."""
+    members only (non-members do not participate), bootstrapped through the default store -- or carved out
+    of a parent communicator with ``ncclCommSplit`` (``NativeGroup.split``, how 2-D meshes are built)."""
 
-    def __init__(self, ranks: list[int], tag: str, device: torch.device, store=None, priority: int = 0):
+    def __init__(self, ranks: list[int], tag: str, device: torch.device, store=None, priority: int = 0,
+                 _comm: int | None = None):
         self.ranks = list(ranks)
         me = dist.get_rank()
         if me not in self.ranks:
             raise ValueError("NativeGroup built on a non-member rank")
         self.rank, self._size = self.ranks.index(me), len(self.ranks)
         self.device = device
-        store = store or dist.distributed_c10d._get_default_store()
-        key = f"dllm/rccl/{tag}/{'-'.join(map(str, self.ranks))}"
-        nbytes = _lib().dllm_nccl_unique_id_bytes()
-        if self.rank == 0:
-            buf = ctypes.create_string_buffer(nbytes)
-            _check(_lib().dllm_nccl_unique_id(buf, nbytes), "ncclGetUniqueId")
-            uid = buf.raw
-            store.set(key, uid)
-        else:
-            uid = store.get(key)
-        comm = ctypes.c_void_p()
-        _check(_lib().dllm_nccl_comm_init(self._size, self.rank, uid, device.index, ctypes.byref(comm)),
-               "ncclCommInitRank")
-        self.comm = comm.value
+        if _comm is None:
+            store = store or dist.distributed_c10d._get_default_store()
+            key = f"dllm/rccl/{tag}/{'-'.join(map(str, self.ranks))}"
+            nbytes = _lib().dllm_nccl_unique_id_bytes()
+            if self.rank == 0:
+                buf = ctypes.create_string_buffer(nbytes)
+                _check(_lib().dllm_nccl_unique_id(buf, nbytes), "ncclGetUniqueId")
+                uid = buf.raw
+                store.set(key, uid)
+            else:
+                uid = store.get(key)
+            comm = ctypes.c_void_p()
+            _check(_lib().dllm_nccl_comm_init(self._size, self.rank, uid, device.index, ctypes.byref(comm)),
+                   "ncclCommInitRank")
+            _comm = comm.value
+        self.comm = _comm
         st = ctypes.c_void_p()
         _check(_lib().dllm_stream_create(priority, ctypes.byref(st)), "hipStreamCreate")
         self.stream = st.value
+
+    @classmethod
+    def split(cls, parent: "NativeGroup", groups: list[list[int]], device: torch.device) -> "NativeGroup | None":
+        """``ncclCommSplit`` of ``parent`` into ``groups`` (lists of global ranks, disjoint): collective over
+        ALL of the parent's ranks; returns this rank's new group (its own communicator and stream), or None
+        if this rank is in none of them (it passes NCCL_SPLIT_NOCOLOR)."""
+        me = dist.get_rank()
+        color, mine = NCCL_SPLIT_NOCOLOR, None
+        for i, g in enumerate(groups):
+            if me in g:
+                color, mine = i, g
+        comm = ctypes.c_void_p()
+        _check(_lib().dllm_nccl_comm_split(parent.comm, color, mine.index(me) if mine else 0, ctypes.byref(comm)),
+               "ncclCommSplit")
+        if mine is None:
+            return None
+        return cls(mine, "split", device, _comm=comm.value)
 
     def size(self) -> int:
         return self._size
@@ -172,6 +196,53 @@ class NativeGroup:
 
         return self._enqueue(run, (out, full))
 
+    # -- grouped collectives (ncclGroupStart/End: one fused launch, one completion event) ---------------
+    def _enqueue_group(self, calls, keep):
+        cur = torch.cuda.current_stream(self.device).cuda_stream
+        ev_in = _Event()
+        _check(_lib().dllm_event_record(ev_in.h, cur), "hipEventRecord")
+        _check(_lib().dllm_stream_wait_event(self.stream, ev_in.h), "hipStreamWaitEvent")
+        _check(_lib().dllm_nccl_group_start(), "ncclGroupStart")
+        try:
+            for fn in calls:
+                fn(self.stream)
+        finally:
+            # the collectives are launched at GroupEnd, so the completion event is recorded after it
+            _check(_lib().dllm_nccl_group_end(), "ncclGroupEnd")
+        ev_out = _Event()
+        _check(_lib().dllm_event_record(ev_out.h, self.stream), "hipEventRecord")
+        return NativeWork(ev_out, keep=(ev_in,) + tuple(keep))
+
+    def all_gather_into_many(self, pairs) -> NativeWork:
+        """Several all-gathers ``(out, shard)`` as one group (e.g. a layer's W1 and W2 shards)."""
+        calls, keep = [], []
+        for out, shard in pairs:
+            if out.numel() != shard.numel() * self._size:
+                raise ValueError("all_gather_into_many: size mismatch")
+
+            def run(s, out=out, shard=shard):
+                _check(_lib().dllm_nccl_all_gather(self.comm, shard.data_ptr(), out.data_ptr(), shard.numel(),
+                                                   _DT[shard.dtype], s), "ncclAllGather")
+
+            calls.append(run)
+            keep += [out, shard]
+        return self._enqueue_group(calls, keep)
+
+    def reduce_scatter_into_many(self, pairs) -> NativeWork:
+        """Several reduce-scatters ``(out, full)`` as one group (a layer's W1 and W2 gradients)."""
+        calls, keep = [], []
+        for out, full in pairs:
+            if full.numel() != out.numel() * self._size:
+                raise ValueError("reduce_scatter_into_many: size mismatch")
+
+            def run(s, out=out, full=full):
+                _check(_lib().dllm_nccl_reduce_scatter(self.comm, full.data_ptr(), out.data_ptr(), out.numel(),
+                                                       _DT[full.dtype], s), "ncclReduceScatter")
+
+            calls.append(run)
+            keep += [out, full]
+        return self._enqueue_group(calls, keep)
+
     def check_async_error(self) -> None:
         _check(_lib().dllm_nccl_comm_async_error(self.comm), "ncclCommGetAsyncError")
 
@@ -196,3 +267,8 @@ def new_role_group(ranks: list[int], role: str, device: torch.device) -> NativeG
     if dist.get_rank() not in ranks:
         return None
     return NativeGroup(ranks, f"{role}/{next(_COUNTER)}", device)
+
+
+def new_world_group(device: torch.device) -> NativeGroup:
+    """The job-wide communicator every mesh communicator is split from (collective over all ranks)."""
+    return NativeGroup(list(range(dist.get_world_size())), f"world/{next(_COUNTER)}", device)

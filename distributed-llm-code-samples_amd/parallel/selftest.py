@@ -52,6 +52,21 @@ def check_collectives(mesh: Mesh, device, n: int = 128) -> None:
     comm.reduce_scatter_into(o, big[rank], grp, async_op=True).wait()
     want = torch.stack(big).sum(0)[rank * n:(rank + 1) * n]
     assert torch.allclose(o.cpu(), want.cpu()), "reduce_scatter mismatch"
+    # grouped collectives (a layer's W2 + W1 pair, two different sizes, issued as one group): each output
+    # must match its own collective, in order
+    outs = [torch.zeros(n * world, device=device), torch.zeros(2 * n * world, device=device)]
+    ins = [mine, _input(rank + 77, 2 * n, device)]
+    comm.all_gather_into_many(list(zip(outs, ins)), grp, async_op=True).wait()
+    assert torch.equal(outs[0].cpu(), torch.cat(allin).cpu()), "all_gather_into_many[0] mismatch"
+    assert torch.equal(outs[1].cpu(), torch.cat([_input(r + 77, 2 * n, device) for r in range(world)]).cpu()), \
+        "all_gather_into_many[1] mismatch"
+    fulls = [big[rank], _input(rank + 99, 2 * n * world, device)]
+    os_ = [torch.zeros(n, device=device), torch.zeros(2 * n, device=device)]
+    comm.reduce_scatter_into_many(list(zip(os_, fulls)), grp, async_op=True).wait()
+    assert torch.allclose(os_[0].cpu(), want.cpu()), "reduce_scatter_into_many[0] mismatch"
+    want1 = torch.stack([_input(r + 99, 2 * n * world, device) for r in range(world)]).sum(0)
+    assert torch.allclose(os_[1].cpu(), want1[rank * 2 * n:(rank + 1) * 2 * n].cpu()), \
+        "reduce_scatter_into_many[1] mismatch"
     # role groups of a dp x tp mesh
     for role in ("dp_ar", "dp_ag", "dp_rs", "tp"):
         g = mesh.group(role)
@@ -61,6 +76,18 @@ def check_collectives(mesh: Mesh, device, n: int = 128) -> None:
         t = mine.clone()
         comm.all_reduce(t, g).wait()
         assert torch.allclose(t.cpu(), sum(allin[r] for r in ranks).cpu()), f"{role} all_reduce mismatch"
+        # grouped pair on the role communicator (native: ncclGroupStart/End around both)
+        k, me = len(ranks), ranks.index(rank)
+        ag = [torch.zeros(n * k, device=device), torch.zeros(2 * n * k, device=device)]
+        comm.all_gather_into_many([(ag[0], mine), (ag[1], ins[1])], g).wait()
+        assert torch.equal(ag[0].cpu(), torch.cat([allin[r] for r in ranks]).cpu()), f"{role} grouped AG"
+        rs = [torch.zeros(n // k if n % k == 0 else n, device=device) for _ in range(2)]
+        if n % k == 0:
+            comm.reduce_scatter_into_many([(rs[0], mine), (rs[1], mine * 2)], g).wait()
+            tot = sum(allin[r] for r in ranks)
+            seg = slice(me * (n // k), (me + 1) * (n // k))
+            assert torch.allclose(rs[0].cpu(), tot[seg].cpu()) and torch.allclose(rs[1].cpu(), 2 * tot[seg].cpu()), \
+                f"{role} grouped RS"
 
 
 def check_async_side_stream(world: int, device, iters: int = 10) -> None:
