@@ -1,0 +1,6 @@
+#!/bin/bash
+# fp32 256x256 LDS-DMA kernel: numerics + throughput vs torch (hipBLASLt); native RCCL split/grouped comm tests
+source scripts/gpu_steps.sh
+step test_fp32 600 python -u -m pytest tests/test_gemm_gpu.py -x -q -k "fp32" --timeout 120 --timeout-method thread
+step test_comm 600 python -u -m pytest tests/test_comm_gpu.py -x -q --timeout 120 --timeout-method thread
+step bench_fp32 300 python scripts/bench_fp32.py

@@ -187,6 +187,13 @@ def test_zero2_shards_fp32_state(free_port):
     st = r["state_numel"]
     assert st["master"] * 4 == st["total"] and st["adam"] == st["master"]
     assert st["copy"] == st["total"] and st["grads"] == st["total"]
+    from dllm.utils.sizing import plan
+
+    pz = plan(64, 256, 2, 16, dp=4, mode="zero", dtype="fp32", grad_dtype="fp32", optimizer="adam")["bytes"]
+    assert pz["master_fp32"] == 4 * st["master"] and pz["adam_moments"] == 8 * st["adam"]
+    r_f = _run(cfg, 3, 4, free_port + 2, rec=True)  # FSDP: everything is a 1/dp row shard
+    pf = plan(64, 256, 2, 16, dp=4, mode="fsdp", dtype="fp32", grad_dtype="fp32", optimizer="adam")["bytes"]
+    assert pf["master_fp32"] == 4 * r_f["state_numel"]["master"] == 4 * r_f["state_numel"]["total"]
     _close(r["params"], _run(cfg, 2, 4, free_port + 1), rtol=1e-6, atol=1e-8)  # == DDP
 
 

@@ -65,3 +65,28 @@ def test_fused_optimizer_equals_unfused(opt):
     for g, w in zip(a, b):
         for k in w:
             torch.testing.assert_close(g[k], w[k], rtol=1e-6, atol=1e-8)
+
+
+@pytest.mark.parametrize("gated,act,opt,rec", [(False, "relu", "sgd", "none"), (True, "silu", "adam", "none"),
+                                               (False, "gelu", "adam", "full")])
+def test_sizing_plan_matches_engine_buffers(gated, act, opt, rec):
+    """utils/sizing.plan (the README's per-rank HBM table) predicts the engine's own allocations."""
+    from dllm.parallel.engine import FFNTrainer
+    from dllm.parallel.mesh import Mesh
+    from dllm.utils.config import ModelConfig, TrainConfig
+    from dllm.utils.sizing import plan
+
+    m = ModelConfig(64, 192, 3, act, gated)
+    cfg = TrainConfig(model=m, batch_size=2, seq_len=64, dtype="bf16", grad_dtype="bf16", optimizer=opt,
+                      recompute=rec)
+    eng = FFNTrainer(cfg, Mesh(), "cpu")
+    p = plan(64, 192, 3, 128, gated=gated, act=act, dtype="bf16", grad_dtype="bf16", optimizer=opt, recompute=rec,
+             relu_mask=False)["bytes"]
+    nb = lambda t: t.numel() * t.element_size()  # noqa: E731
+    assert p["master_fp32"] == nb(eng.master) and p["compute_copy"] == nb(eng.copy) and p["grads"] == nb(eng.grads)
+    if opt == "adam":
+        assert p["adam_moments"] == nb(eng.adam_m) + nb(eng.adam_v)
+    assert p["layer_inputs"] == sum(nb(t) for t in eng.xs[1:]) + 128 * 64 * 2
+    assert p["activations"] == sum(nb(t) for t in eng.acts_a)
+    assert p.get("preactivations", 0) == (sum(nb(t) for t in eng.acts_h) if eng.acts_h else 0)
+    assert p["dgrad_buffer"] == nb(eng.da) and p["dx_buffers"] == sum(nb(t) for t in eng.dxb)

@@ -135,13 +135,47 @@ def test_gated_epilogues(dtype, variant):
 
 
 @pytest.mark.parametrize("layout", ["nt", "nn", "tn"])
-def test_fp32_mfma_exact_f32(layout):
-    M, N, K = 256, 384, 272
+@pytest.mark.parametrize("M,N,K", [(256, 384, 272), (512, 768, 272), (256, 256, 16), (768, 512, 48)])
+def test_fp32_mfma_exact_f32(layout, M, N, K):
+    """Exact-fp32 MFMA paths: the 128x128 kernel (N % 256 != 0) and the 256x256 LDS-DMA kernel (3-stage ring,
+    K permutation; nk = 17 / 1 / 3 cover the ring's prologue and tail waits)."""
     a, b = _operands(layout, M, N, K, torch.float32, seed=3)
     assert gemm_path(torch.float32, torch.float32, M, N, K, a.stride(0), b.stride(0), N) == "mfma_f32"
     out = gemm(a.to(DEV), b.to(DEV), layout, force="mfma_f32").cpu().double()
     ref = _ref(a, b, layout)
     assert ((out - ref).abs().max() / ref.abs().max()) < 1e-6
+
+
+@pytest.mark.parametrize("epi", ["act", "dact", "sgd", "adam", "glu", "beta"])
+def test_fp32_256_epilogues(epi):
+    """The 256x256 fp32 kernel's fused epilogues (shared with the bf16 8-phase kernel) vs the torch oracle."""
+    M, N, K = 512, 512, 256
+    layout = {"act": "nt", "dact": "nn", "sgd": "tn", "adam": "tn", "glu": "nt", "beta": "nt"}[epi]
+    a, b = _operands(layout, M, N, K, torch.float32, seed=13)
+    kw = {}
+    out = _mk((M, N // 2 if epi == "glu" else N), torch.float32, 14)
+    if epi == "act":
+        kw = dict(epi="act", act="gelu", aux_out=torch.zeros(M, N))
+    elif epi == "dact":
+        kw = dict(epi="dact", act="silu", aux=_mk((M, N), torch.float32, 15))
+    elif epi == "glu":
+        kw = dict(epi="glu", act="silu", aux_out=torch.zeros(M, N))
+    elif epi == "beta":
+        kw = dict(beta=0.5, alpha=2.0)
+    elif epi in ("sgd", "adam"):
+        kw = dict(epi=epi, lr=1e-2)
+        if epi == "adam":
+            kw.update(step=3, opt_m=torch.full((M, N), 0.01), opt_v=torch.full((M, N), 1e-4))
+    want_out = out.clone()
+    want_kw = {k: (v.clone() if isinstance(v, torch.Tensor) else v) for k, v in kw.items()}
+    gemm(a, b, layout, out=want_out, **want_kw)  # CPU: the torch oracle
+    got_kw = {k: (v.to(DEV) if isinstance(v, torch.Tensor) else v) for k, v in kw.items()}
+    got_out = out.to(DEV)
+    gemm(a.to(DEV), b.to(DEV), layout, out=got_out, **got_kw)
+    torch.testing.assert_close(got_out.cpu(), want_out, rtol=1e-5, atol=1e-5)
+    for k, v in got_kw.items():
+        if isinstance(v, torch.Tensor) and k in ("aux_out", "opt_m", "opt_v"):
+            torch.testing.assert_close(v.cpu(), want_kw[k], rtol=1e-5, atol=1e-5)
 
 
 @pytest.mark.parametrize("layout", ["nt", "nn", "tn"])
