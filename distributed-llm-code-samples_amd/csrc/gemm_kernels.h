@@ -1260,28 +1260,29 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_128(GemmArgs p) {
 }
 
 // ----------------------------------------------------------------------------------------------
-// fp32 256x256x16 MFMA kernel (reference-precision path: exact-fp32 v_mfma_f32_16x16x4_f32)
+// fp32 256x256x32 MFMA kernel (reference-precision path: exact-fp32 v_mfma_f32_16x16x4_f32)
 //
 // The fp32 MFMA is 4x slower per FLOP than bf16 (157 TF peak), so each 16x16x4 MFMA is 32 cycles and the LDS
 // traffic per MFMA is small; what caps an fp32 GEMM is feeding the MFMA pipe without gaps: here 8 waves (2M x 4N,
-// 2 per SIMD), a 256x256 block tile (half the operand bytes per FLOP of a 128x128 tile), a 3-stage LDS ring
-// filled by LDS-DMA (global_load_lds_dwordx4) two K-tiles ahead, ONE barrier per 16-deep K-tile (128 MFMAs =
-// 4096 cycles per wave between barriers), and counted vmcnt waits (never 0 in the loop).
+// 2 per SIMD), a 256x256 block tile (half the operand bytes per FLOP of a 128x128 tile), K-tiles of 32 (128-B
+// rows: every LDS-DMA touches whole cache lines), a 2-stage LDS ring (128 KiB) filled by LDS-DMA
+// (global_load_lds_dwordx4) one K-tile ahead, and ONE barrier per K-tile (256 MFMAs = 8192 cycles per wave
+// between barriers, far longer than the DMA latency it hides).
 //
-// K permutation: an MFMA consumes k = kk (lane group l/16) of its 4; lane group g supplies k = 4g + s at step s
-// for both operands, so a K-contiguous fragment is ONE ds_read_b128 (A[row][4g .. 4g+3]) serving all 4 steps.
-// (The sum over k is order-independent in exact arithmetic; the fp32 result is exact per product, rounded in
-// a different summation order than a k-sequential chain -- like any blocked BLAS.)
-// LDS images (conflict-free):  K-contiguous [256 rows][16 k] (64 B rows), 16-B chunk ^= (row >> 2) & 3;
-//                              MN-contiguous [16 k][256 mn] (1 KiB rows), mn ^= ((k >> 2) & 3) << 4.
+// K permutation: an MFMA consumes k = kk (lane group l/16) of its 4; at step s (0..7) lane group g supplies
+// k = 8g + s for BOTH operands, so a K-contiguous fragment is two ds_read_b128 (A[row][8g .. 8g+7]) serving all
+// 8 steps.  (Exact products; the fp32 sums run in a different order than a k-sequential chain -- like any
+// blocked BLAS.)  Each K-tile is consumed in two halves (steps 0-3, 4-7) to keep the fragment registers at 48.
+// LDS images (conflict-free):  K-contiguous [256 rows][32 k] (128-B rows), 16-B chunk ^= (row >> 1) & 7;
+//                              MN-contiguous [32 k][256 mn] (1 KiB rows), mn ^= ((k >> 3) & 3) << 4.
 // The per-wave tile follows the 8-phase bf16 kernel's quadrant map, so its batched epilogues (act, dact,
 // glu, dglu, sgd, adam, store) are reused as is.
 // ----------------------------------------------------------------------------------------------
-constexpr int F2_T = 256, F2_K = 16, F2_STAGE = 2 * F2_T * F2_K * 4;  // 32 KiB per stage (A + B)
+constexpr int F2_T = 256, F2_K = 32, F2_HALF = F2_T * F2_K * 4, F2_STAGE = 2 * F2_HALF;  // 64 KiB per stage
 
 template <int LAYOUT, int EPI>
 __global__ __launch_bounds__(512, 1) void gemm_f32_256(GemmArgs p) {
-  __shared__ __attribute__((aligned(16))) char smem[3 * F2_STAGE];
+  __shared__ __attribute__((aligned(16))) char smem[2 * F2_STAGE];
   DLLM_LDS char* lds = (DLLM_LDS char*)smem;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1298,48 +1299,47 @@ __global__ __launch_bounds__(512, 1) void gemm_f32_256(GemmArgs p) {
   const float* B = (const float*)p.B + (B_KC ? (long)n0 * p.ldb : (long)n0);
   const long a_kstep = A_KC ? F2_K : (long)F2_K * p.lda;
   const long b_kstep = B_KC ? F2_K : (long)F2_K * p.ldb;
-  // LDS-DMA: the 16 KiB operand tile is 16 pieces of 1 KiB (64 lanes x 16 B, lane-linear); wave w fills pieces
-  // w and w + 8.  Per-lane element offsets of the source (the swizzle is applied on the source address).
-  long aoff[2], boff[2];
-  auto kc_off = [&](long ld, long (&o)[2]) {
+  // LDS-DMA: the 32 KiB operand tile is 32 pieces of 1 KiB (64 lanes x 16 B, lane-linear); wave w fills pieces
+  // w, w+8, w+16, w+24.  Per-lane 32-bit byte offsets of the source (the swizzle is applied on the source).
+  uint32_t aoff[4], boff[4];
+  auto kc_off = [&](long ld, uint32_t (&o)[4]) {  // piece q = rows 8q .. 8q+7 (128 B each)
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int q = wid + 8 * i, row = 16 * q + (lane >> 2);
-      o[i] = (long)row * ld + 4 * ((lane & 3) ^ ((row >> 2) & 3));
+    for (int i = 0; i < 4; ++i) {
+      const int q = wid + 8 * i, row = 8 * q + (lane >> 3);
+      o[i] = (uint32_t)(((long)row * ld + 4 * ((lane & 7) ^ ((row >> 1) & 7))) * 4);
     }
   };
-  auto mc_off = [&](long ld, long (&o)[2]) {
+  auto mc_off = [&](long ld, uint32_t (&o)[4]) {  // piece q = k row q (1 KiB)
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < 4; ++i) {
       const int k = wid + 8 * i;
-      o[i] = (long)k * ld + ((4 * lane) ^ (((k >> 2) & 3) << 4));
+      o[i] = (uint32_t)(((long)k * ld + ((4 * lane) ^ (((k >> 3) & 3) << 4))) * 4);
     }
   };
   if constexpr (A_KC) kc_off(p.lda, aoff); else mc_off(p.lda, aoff);
   if constexpr (B_KC) kc_off(p.ldb, boff); else mc_off(p.ldb, boff);
   auto stage = [&](int kt, int buf) {
     DLLM_LDS char* As = lds + buf * F2_STAGE;
-    DLLM_LDS char* Bs = As + F2_STAGE / 2;
-    const float* a = A + kt * a_kstep;
-    const float* b = B + kt * b_kstep;
+    DLLM_LDS char* Bs = As + F2_HALF;
+    const char* a = (const char*)(A + kt * a_kstep);
+    const char* b = (const char*)(B + kt * b_kstep);
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 4; ++i)
       __builtin_amdgcn_global_load_lds((const DLLM_GLB void*)(a + aoff[i]), (DLLM_LDS void*)(As + (wid + 8 * i) * 1024),
                                        16, 0, 0);
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 4; ++i)
       __builtin_amdgcn_global_load_lds((const DLLM_GLB void*)(b + boff[i]), (DLLM_LDS void*)(Bs + (wid + 8 * i) * 1024),
                                        16, 0, 0);
   };
-  // fragment byte offsets inside a stage's A / B tile.  Row tiles of the wave: r = QM*128 + wr*64 + mt*16
-  // (QM, mt) -> index QM*4 + mt; column tiles c = QN*128 + wc*32 + nt*16 -> QN*2 + nt.
+  // fragment byte offsets.  Row tiles of the wave: r = QM*128 + wr*64 + mt*16 -> index QM*4 + mt; column tiles
+  // c = QN*128 + wc*32 + nt*16 -> QN*2 + nt (the bf16 8-phase kernel's quadrant map).
   const int g = lane >> 4, i15 = lane & 15;
-  auto kc_addr = [&](int r0) {  // ds_read_b128: [row][k 4g..4g+3]
+  auto kc_addr = [&](int r0, int h) {  // ds_read_b128: [row][k 8g + 4h .. +3]
     const int row = r0 + i15;
-    return (uint32_t)(row * 64 + ((g ^ ((row >> 2) & 3)) << 4));
+    return (uint32_t)(row * 128 + (((2 * g + h) ^ ((row >> 1) & 7)) << 4));
   };
-  auto mc_addr = [&](int c0, int s) {  // ds_read_b32: [k = 4g + s][mn]
-    const int k = 4 * g + s;
+  auto mc_addr = [&](int c0, int k) {  // ds_read_b32: [k][mn]
     return (uint32_t)(k * 1024 + (((c0 + i15) ^ (g << 4)) << 2));
   };
   f32x4_t acc[2][2][4][2];
@@ -1354,49 +1354,50 @@ __global__ __launch_bounds__(512, 1) void gemm_f32_256(GemmArgs p) {
 
   const int nk = p.K / F2_K;
   stage(0, 0);
-  if (nk > 1) stage(1, 1);
   for (int kt = 0; kt < nk; ++kt) {
-    // stage kt landed (the one younger stage, 4 loads, may stay in flight); the barrier publishes it to all
-    // waves and retires every wave's reads of buffer (kt + 2) % 3 (iteration kt - 1) before it is restaged
-    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // stage kt landed; the barrier publishes it to every wave and retires every wave's reads of the other
+    // buffer (iteration kt - 1) before it is restaged with K-tile kt + 1
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (kt + 2 < nk) stage(kt + 2, (kt + 2) % 3);
-    const DLLM_LDS char* As = lds + (kt % 3) * F2_STAGE;
-    const DLLM_LDS char* Bs = As + F2_STAGE / 2;
-    float af[8][4], bf[4][4];  // [row tile][step], [col tile][step]
+    if (kt + 1 < nk) stage(kt + 1, (kt + 1) & 1);
+    const DLLM_LDS char* As = lds + (kt & 1) * F2_STAGE;
+    const DLLM_LDS char* Bs = As + F2_HALF;
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      const int r0 = (t >> 2) * 128 + wr * 64 + (t & 3) * 16;
-      if constexpr (A_KC) {
-        const f32x4_t v = *(const DLLM_LDS f32x4_t*)(As + kc_addr(r0));
-        af[t][0] = v[0]; af[t][1] = v[1]; af[t][2] = v[2]; af[t][3] = v[3];
-      } else {
+    for (int h = 0; h < 2; ++h) {
+      float af[8][4], bf[4][4];  // [row tile][step], [col tile][step]
 #pragma unroll
-        for (int s2 = 0; s2 < 4; ++s2) af[t][s2] = *(const DLLM_LDS float*)(As + mc_addr(r0, s2));
+      for (int t = 0; t < 8; ++t) {
+        const int r0 = (t >> 2) * 128 + wr * 64 + (t & 3) * 16;
+        if constexpr (A_KC) {
+          const f32x4_t v = *(const DLLM_LDS f32x4_t*)(As + kc_addr(r0, h));
+          af[t][0] = v[0]; af[t][1] = v[1]; af[t][2] = v[2]; af[t][3] = v[3];
+        } else {
+#pragma unroll
+          for (int s2 = 0; s2 < 4; ++s2) af[t][s2] = *(const DLLM_LDS float*)(As + mc_addr(r0, 8 * g + 4 * h + s2));
+        }
       }
-    }
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int c0 = (t >> 1) * 128 + wc * 32 + (t & 1) * 16;
-      if constexpr (B_KC) {
-        const f32x4_t v = *(const DLLM_LDS f32x4_t*)(Bs + kc_addr(c0));
-        bf[t][0] = v[0]; bf[t][1] = v[1]; bf[t][2] = v[2]; bf[t][3] = v[3];
-      } else {
+      for (int t = 0; t < 4; ++t) {
+        const int c0 = (t >> 1) * 128 + wc * 32 + (t & 1) * 16;
+        if constexpr (B_KC) {
+          const f32x4_t v = *(const DLLM_LDS f32x4_t*)(Bs + kc_addr(c0, h));
+          bf[t][0] = v[0]; bf[t][1] = v[1]; bf[t][2] = v[2]; bf[t][3] = v[3];
+        } else {
 #pragma unroll
-        for (int s2 = 0; s2 < 4; ++s2) bf[t][s2] = *(const DLLM_LDS float*)(Bs + mc_addr(c0, s2));
+          for (int s2 = 0; s2 < 4; ++s2) bf[t][s2] = *(const DLLM_LDS float*)(Bs + mc_addr(c0, 8 * g + 4 * h + s2));
+        }
       }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            acc[t >> 2][u >> 1][t & 3][u & 1] =
+                __builtin_amdgcn_mfma_f32_16x16x4f32(bf[u][s2], af[t][s2], acc[t >> 2][u >> 1][t & 3][u & 1], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
     }
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s2 = 0; s2 < 4; ++s2)
-#pragma unroll
-      for (int t = 0; t < 8; ++t)
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          acc[t >> 2][u >> 1][t & 3][u & 1] =
-              __builtin_amdgcn_mfma_f32_16x16x4f32(bf[u][s2], af[t][s2], acc[t >> 2][u >> 1][t & 3][u & 1], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
   }
   epilogue_256<EPI, float, -1>(p, acc, m0, n0, wr, wc, lane, p.C);
 }

@@ -135,10 +135,10 @@ def test_gated_epilogues(dtype, variant):
 
 
 @pytest.mark.parametrize("layout", ["nt", "nn", "tn"])
-@pytest.mark.parametrize("M,N,K", [(256, 384, 272), (512, 768, 272), (256, 256, 16), (768, 512, 48)])
+@pytest.mark.parametrize("M,N,K", [(256, 384, 272), (512, 768, 288), (256, 256, 32), (768, 512, 96)])
 def test_fp32_mfma_exact_f32(layout, M, N, K):
-    """Exact-fp32 MFMA paths: the 128x128 kernel (N % 256 != 0) and the 256x256 LDS-DMA kernel (3-stage ring,
-    K permutation; nk = 17 / 1 / 3 cover the ring's prologue and tail waits)."""
+    """Exact-fp32 MFMA paths: the 128x128 kernel (N % 256 != 0) and the 256x256 LDS-DMA kernel (2-stage ring,
+    K permutation; nk = 9 / 1 / 3 cover the ring's prologue and tail)."""
     a, b = _operands(layout, M, N, K, torch.float32, seed=3)
     assert gemm_path(torch.float32, torch.float32, M, N, K, a.stride(0), b.stride(0), N) == "mfma_f32"
     out = gemm(a.to(DEV), b.to(DEV), layout, force="mfma_f32").cpu().double()
@@ -172,10 +172,12 @@ def test_fp32_256_epilogues(epi):
     got_kw = {k: (v.to(DEV) if isinstance(v, torch.Tensor) else v) for k, v in kw.items()}
     got_out = out.to(DEV)
     gemm(a.to(DEV), b.to(DEV), layout, out=got_out, **got_kw)
-    torch.testing.assert_close(got_out.cpu(), want_out, rtol=1e-5, atol=1e-5)
+    tol = 1e-4 if epi in ("act", "glu") else 1e-5  # device GELU/SiLU vs torch's: a few fp32 ulps
+    torch.testing.assert_close(got_out.cpu(), want_out, rtol=tol, atol=tol)
     for k, v in got_kw.items():
         if isinstance(v, torch.Tensor) and k in ("aux_out", "opt_m", "opt_v"):
-            torch.testing.assert_close(v.cpu(), want_kw[k], rtol=1e-5, atol=1e-5)
+            w = want_kw[k]
+            torch.testing.assert_close(v.cpu(), w, rtol=1e-5, atol=1e-6 * float(w.abs().max()) + 1e-12)
 
 
 @pytest.mark.parametrize("layout", ["nt", "nn", "tn"])
