@@ -64,11 +64,11 @@ def _headers_mtime() -> float:
 COMMON_FLAGS = ["-O3", "-fPIC", "-std=c++20", f"--offload-arch={ARCH}", "-Wno-unused-result"]
 
 
-def _compile(src: str, verbose: bool) -> str:
-    obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+def _compile(src: str, verbose: bool, build_dir: str = BUILD, extra: tuple = ()) -> str:
+    obj = os.path.join(build_dir, os.path.basename(src) + ".o")
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), _headers_mtime()):
         return obj
-    cmd = [_hipcc(), *COMMON_FLAGS, "-I", CSRC, f"-I{ROCM}/include", "-c", src, "-o", obj]
+    cmd = [_hipcc(), *COMMON_FLAGS, *extra, "-I", CSRC, f"-I{ROCM}/include", "-c", src, "-o", obj]
     if src.endswith(".cpp"):
         cmd.insert(1, "-x")
         cmd.insert(2, "hip")
@@ -109,22 +109,29 @@ def build_tools(verbose: bool = False, force: bool = False) -> list[str]:
     return out
 
 
-def build(verbose: bool = False, force: bool = False, jobs: int = 0) -> str:
-    """Compile all native sources for gfx950 and link ``_dllm_native.so``; returns the library path."""
-    os.makedirs(BUILD, exist_ok=True)
+def build(verbose: bool = False, force: bool = False, jobs: int = 0, variant: str = "", defines: tuple = ()) -> str:
+    """Compile all native sources for gfx950 and link ``_dllm_native.so``; returns the library path.
+
+    ``variant`` + ``defines`` (A/B experiments only): build into ``build_<variant>/`` with extra ``-D`` flags and
+    link ``_dllm_native_<variant>.so`` next to the production library; load it with ``DLLM_NATIVE_LIB``."""
+    build_dir = BUILD + (f"_{variant}" if variant else "")
+    lib_path = LIB_PATH.replace(".so", f"_{variant}.so") if variant else LIB_PATH
+    extra = tuple(f"-D{d}" for d in defines)
+    os.makedirs(build_dir, exist_ok=True)
     if force:
-        for f in os.listdir(BUILD):
-            os.remove(os.path.join(BUILD, f))
-    build_tools(verbose, force)
+        for f in os.listdir(build_dir):
+            os.remove(os.path.join(build_dir, f))
+    if not variant:
+        build_tools(verbose, force)
     srcs = sources()
     jobs = jobs or min(8, os.cpu_count() or 4, len(srcs))  # the GEMM library is split per layout for this
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        objs = list(ex.map(lambda s: _compile(s, verbose), srcs))
+        objs = list(ex.map(lambda s: _compile(s, verbose, build_dir, extra), srcs))
     newest = max(os.path.getmtime(o) for o in objs)
-    if not force and os.path.exists(LIB_PATH) and os.path.getmtime(LIB_PATH) >= newest:
-        return LIB_PATH
+    if not force and os.path.exists(lib_path) and os.path.getmtime(lib_path) >= newest:
+        return lib_path
     tdir = _torch_lib_dir()
-    link = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", LIB_PATH + ".tmp"]
+    link = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", lib_path + ".tmp"]
     if tdir and os.path.exists(os.path.join(tdir, "librccl.so")):
         # bind RCCL to torch's bundled copy (same SONAME librccl.so.1 as /opt/rocm's)
         link += [f"-L{tdir}", "-l:librccl.so", f"-Wl,-rpath,{tdir}"]
@@ -135,9 +142,12 @@ def build(verbose: bool = False, force: bool = False, jobs: int = 0) -> str:
     r = subprocess.run(link, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
-    os.replace(LIB_PATH + ".tmp", LIB_PATH)
-    return LIB_PATH
+    os.replace(lib_path + ".tmp", lib_path)
+    return lib_path
 
 
 if __name__ == "__main__":
-    print(build(verbose="-v" in sys.argv, force="-f" in sys.argv))
+    # python -m dllm._build [-v] [-f] [--variant NAME -DMACRO=VAL ...]
+    var = sys.argv[sys.argv.index("--variant") + 1] if "--variant" in sys.argv else ""
+    defs = tuple(a[2:] for a in sys.argv if a.startswith("-D"))
+    print(build(verbose="-v" in sys.argv, force="-f" in sys.argv, variant=var, defines=defs))

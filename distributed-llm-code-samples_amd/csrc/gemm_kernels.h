@@ -29,6 +29,12 @@
 #include <algorithm>
 #include <type_traits>
 
+// MFMA-cluster wave priority of the 8-phase kernel (build-time experiment knob): 0 = s_setprio(1) around every
+// MFMA cluster (default), 1 = static prio 1 for waves 4-7 only, 2 = none
+#ifndef DLLM_PRIO_MODE
+#define DLLM_PRIO_MODE 0
+#endif
+
 #include "common.h"
 
 namespace dllm {
@@ -988,7 +994,9 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
     }
   };
   auto mfma_quad = [&](f32x4_t (&c)[4][2], const bf16x8_t (&fb)[2][2]) {
+#if DLLM_PRIO_MODE == 0
     __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
@@ -996,8 +1004,15 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt)
           c[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[nt][s2], fa[mt][s2], c[mt][nt], 0, 0, 0);
+#if DLLM_PRIO_MODE == 0
     __builtin_amdgcn_s_setprio(0);
+#endif
   };
+#if DLLM_PRIO_MODE == 1
+  // static priority for the younger (second-dispatched) half, set once (MI355X_MICROARCH.md, two waves per SIMD
+  // item 4) instead of raising every wave's priority around each MFMA cluster
+  if (wr == 1) __builtin_amdgcn_s_setprio(1);
+#endif
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
 
