@@ -34,6 +34,10 @@
 #ifndef DLLM_PRIO_MODE
 #define DLLM_PRIO_MODE 0
 #endif
+// fp32 path: the 256x256x32 LDS-DMA kernel where shapes allow (1), or always the 128x128 kernel (0)
+#ifndef DLLM_F32_256
+#define DLLM_F32_256 1
+#endif
 
 #include "common.h"
 
@@ -1664,7 +1668,7 @@ static hipError_t launch_bf16(const GemmArgs& a, int out_dt, hipStream_t s) {
 }
 template <int L, int E>
 static hipError_t launch_f32(const GemmArgs& a, hipStream_t s) {
-  if (a.M % F2_T == 0 && a.N % F2_T == 0 && a.K % F2_K == 0) {
+  if (DLLM_F32_256 && a.M % F2_T == 0 && a.N % F2_T == 0 && a.K % F2_K == 0) {
     hipLaunchKernelGGL((gemm_f32_256<L, E>), dim3((a.M / F2_T) * (a.N / F2_T)), dim3(512), 0, s, a);
     return hipGetLastError();
   }

@@ -83,20 +83,29 @@ def test_bf16_gated_engine_tracks_fp32_oracle():
             assert rel < 5e-2, (k, rel.item())
 
 
-def test_adam_engine_matches_oracle():
+@pytest.mark.parametrize("act", ["silu", "gelu"])
+def test_adam_engine_matches_oracle(act):
+    """Fused AdamW (in the weight-gradient GEMM epilogue) vs the fp32 oracle, on smooth activations.  Adam's
+    update m/sqrt(v) is a sign-like function of each gradient element, so a gradient that differs only by
+    summation order can move single elements by ~lr; with ReLU a mask flip wherever h is within rounding of 0
+    (one flip moves a whole dW1 row) then spreads through the next steps, so ReLU + Adam has no elementwise
+    oracle at fp32 rounding (the fp32 ReLU engine is checked with SGD above).  Checked: the update norm to 1e-3
+    and all but 0.5 % of elements to 1e-4 relative."""
     D, F, L, T, lr = 128, 512, 2, 256, 1e-3
-    layers, batches = _setup(D, F, L, T, "relu", False, 3)
-    cfg = TrainConfig(model=ModelConfig(D, F, L), batch_size=1, seq_len=T, dtype="fp32", grad_dtype="fp32",
+    layers, batches = _setup(D, F, L, T, act, False, 3)
+    cfg = TrainConfig(model=ModelConfig(D, F, L, act), batch_size=1, seq_len=T, dtype="fp32", grad_dtype="fp32",
                       lr=lr, optimizer="adam", adam_b2=0.95, skip_input_grad=False)
     eng = FFNTrainer(cfg, Mesh(), torch.device("cuda"))
     eng.load_full_params(layers)
     for x, dy in batches:
         eng.train_step(x.cuda(), dy.cuda())
     got = eng.gather_full_params()
-    want = R.train_adam_single(layers, batches, lr, b2=0.95)
-    for g, w in zip(got, want):
+    want = R.train_adam_single(layers, batches, lr, b2=0.95, act=act)
+    for g, w, p0 in zip(got, want, layers):
         for k in g:
-            torch.testing.assert_close(g[k], w[k], rtol=1e-4, atol=2e-5)
+            dg, dw = g[k].double() - p0[k].double(), w[k].double() - p0[k].double()
+            assert (dg - dw).norm() / dw.norm() < 1e-3, k
+            assert ((dg - dw).abs() > 1e-4 * dw.abs().max()).double().mean() < 5e-3, k
 
 
 @pytest.mark.parametrize("act", ["relu", "gelu"])
