@@ -172,8 +172,10 @@ def test_fp32_256_epilogues(epi):
     got_kw = {k: (v.to(DEV) if isinstance(v, torch.Tensor) else v) for k, v in kw.items()}
     got_out = out.to(DEV)
     gemm(a.to(DEV), b.to(DEV), layout, out=got_out, **got_kw)
-    tol = 1e-4 if epi in ("act", "glu") else 1e-5  # device GELU/SiLU vs torch's: a few fp32 ulps
-    torch.testing.assert_close(got_out.cpu(), want_out, rtol=tol, atol=tol)
+    # summation order differs from torch's (K-permuted exact-fp32 MFMA chain): ~K ulps of the largest value;
+    # device GELU/SiLU vs torch's: a few more
+    tol = 1e-4 if epi in ("act", "glu") else 1e-5
+    torch.testing.assert_close(got_out.cpu(), want_out, rtol=tol, atol=2e-6 * float(want_out.abs().max()) + tol)
     for k, v in got_kw.items():
         if isinstance(v, torch.Tensor) and k in ("aux_out", "opt_m", "opt_v"):
             w = want_kw[k]
