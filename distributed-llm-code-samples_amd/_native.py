@@ -22,6 +22,9 @@ _ERR: str | None = None
 
 c_int, c_long, c_float, c_void_p, c_ull = ctypes.c_int, ctypes.c_long, ctypes.c_float, ctypes.c_void_p, ctypes.c_ulonglong
 
+# bumped with every signature change below (csrc/elementwise.hip dllm_abi_version): a stale library fails loudly
+ABI_VERSION = 3
+
 _SIGS = {
     "dllm_gemm": (c_int, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_long, c_void_p, c_long, c_void_p, c_long,
                           c_void_p, c_void_p, c_long, c_int, c_int, c_int, c_float, c_float, c_int, c_int, c_void_p,
@@ -61,6 +64,9 @@ def _load() -> ctypes.CDLL:
             continue
         f = getattr(lib, name)
         f.restype, f.argtypes = res, args
+    if lib.dllm_abi_version() != ABI_VERSION:
+        raise RuntimeError(f"{path} has C ABI {lib.dllm_abi_version()}, expected {ABI_VERSION}; "
+                           "rebuild with python -m dllm._build -f")
     return lib
 
 

@@ -1,7 +1,7 @@
 """Per-kernel register / scratch / LDS usage of a GEMM translation unit (device-only gfx950 compile + the
 code object's metadata notes): catches spills (private segment > 0) and VGPR blow-ups without a GPU.
 
-    python scripts/kernel_resources.py [gemm_tn.hip] [--filter SUBSTR]
+    python scripts/kernel_resources.py [gemm_tn.hip] [--filter SUBSTR] [-D NAME=VALUE ...]
 """
 import argparse
 import os
@@ -18,11 +18,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("src", nargs="?", default="gemm_tn.hip")
     ap.add_argument("--filter", default="gemm_bf16_8ph")
+    ap.add_argument("-D", action="append", default=[], help="extra preprocessor define (NAME=VALUE)")
     a = ap.parse_args()
     with tempfile.TemporaryDirectory() as d:
         obj = os.path.join(d, "k.o")
         subprocess.run(["hipcc", "-O3", "-std=c++20", "--offload-arch=gfx950", "--cuda-device-only", "--no-gpu-bundle-output", "-c",
-                        "-I", CSRC, os.path.join(CSRC, a.src), "-o", obj], check=True)
+                        *[f"-D{d}" for d in a.D], "-I", CSRC, os.path.join(CSRC, a.src), "-o", obj], check=True)
         notes = subprocess.run([os.path.join(LLVM, "llvm-readelf"), "--notes", obj], capture_output=True,
                                text=True, check=True).stdout
         dem = subprocess.run(["c++filt"], input=notes, capture_output=True, text=True).stdout
