@@ -1292,7 +1292,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_128(GemmArgs p) {
 // k = 8g + s for BOTH operands, so a K-contiguous fragment is two ds_read_b128 (A[row][8g .. 8g+7]) serving all
 // 8 steps.  (Exact products; the fp32 sums run in a different order than a k-sequential chain -- like any
 // blocked BLAS.)  Each K-tile is consumed in two halves (steps 0-3, 4-7) to keep the fragment registers at 48.
-// LDS images (conflict-free):  K-contiguous [256 rows][32 k] (128-B rows), 16-B chunk ^= (row >> 1) & 7;
+// LDS images (conflict-free):  K-contiguous [256 rows][32 k] (128-B rows), 16-B chunk ^= f2_swz(row);
 //                              MN-contiguous [32 k][256 mn] (1 KiB rows), mn ^= ((k >> 3) & 3) << 4.
 // The per-wave tile follows the 8-phase bf16 kernel's quadrant map, so its batched epilogues (act, dact,
 // glu, dglu, sgd, adam, store) are reused as is.
@@ -1321,11 +1321,18 @@ __global__ __launch_bounds__(512, 1) void gemm_f32_256(GemmArgs p) {
   // LDS-DMA: the 32 KiB operand tile is 32 pieces of 1 KiB (64 lanes x 16 B, lane-linear); wave w fills pieces
   // w, w+8, w+16, w+24.  Per-lane 32-bit byte offsets of the source (the swizzle is applied on the source).
   uint32_t aoff[4], boff[4];
+  // K-contiguous image: 16-B chunk c of row r sits at chunk position c ^ f2_swz(r).  The fragment reads take
+  // chunk 2g + h in lane group g (lanes 16g .. 16g+15, rows r0 + (lane & 15)); ds_read_b128 serves lanes in four
+  // 16-lane groups ({0-3,12-15,20-27}, {4-11,16-19,28-31}, +32) that mix rows 0-3/12-15 of one g with rows 4-11
+  // of g +- 1, i.e. chunk positions that differ by XOR 2: f2_swz keeps each group on 16 distinct 16-B slots of
+  // the 256-B bank row.  (The bf16 kernel's (r >> 1) & 7 is conflict-free for its XOR-1 pairing but 2-way here:
+  // SQ_LDS_BANK_CONFLICT was ~8 % of the fp32 kernel's cycles, hipBLASLt's 0.)
+  auto f2_swz = [](int row) { return ((row >> 1) & 7) ^ (((row >> 2) & 1) << 2); };
   auto kc_off = [&](long ld, uint32_t (&o)[4]) {  // piece q = rows 8q .. 8q+7 (128 B each)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int q = wid + 8 * i, row = 8 * q + (lane >> 3);
-      o[i] = (uint32_t)(((long)row * ld + 4 * ((lane & 7) ^ ((row >> 1) & 7))) * 4);
+      o[i] = (uint32_t)(((long)row * ld + 4 * ((lane & 7) ^ f2_swz(row))) * 4);
     }
   };
   auto mc_off = [&](long ld, uint32_t (&o)[4]) {  // piece q = k row q (1 KiB)
@@ -1356,7 +1363,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f32_256(GemmArgs p) {
   const int g = lane >> 4, i15 = lane & 15;
   auto kc_addr = [&](int r0, int h) {  // ds_read_b128: [row][k 8g + 4h .. +3]
     const int row = r0 + i15;
-    return (uint32_t)(row * 128 + (((2 * g + h) ^ ((row >> 1) & 7)) << 4));
+    return (uint32_t)(row * 128 + (((2 * g + h) ^ f2_swz(row)) << 4));
   };
   auto mc_addr = [&](int c0, int k) {  // ds_read_b32: [k][mn]
     return (uint32_t)(k * 1024 + (((c0 + i15) ^ (g << 4)) << 2));
