@@ -247,6 +247,20 @@ class FFNTrainer:
 
                 if relu_mask_supported(T // c, self.F_loc, D, self.cd):
                     self.tp_chunks = c
+        # Sequence-parallel forward chunks: chunk i gathers every rank's i-th sub-slice of its T/tp rows, so the
+        # gathered [T, *] buffers (inputs, activations, dy, partial outputs) hold the full T in a chunk-major row
+        # order -- the same order in the forward, the backward and the ReLU masks; rows are independent in the FFN
+        # and each rank's own T/tp rows keep their order.  The gathers of chunks i+1.. and the reduce-scatter of
+        # chunk i run under chunk i's (i+1's) GEMMs.
+        self.sp_chunks = 1
+        if self.sp and c > 1 and T % (256 * c) == 0 and Tl % c == 0:
+            if self.masks is None:
+                self.sp_chunks = c
+            else:
+                from ..ops.gemm import relu_mask_supported
+
+                if relu_mask_supported(T // c, self.F_loc, D, self.cd):
+                    self.sp_chunks = c
         self._tp_pending = None
         # concurrent weight-gradient stream (single device, fused optimizer, kept activations): the dgrad
         # chain (da, dx) stays on the compute stream, dW2 / dW1 run on a side stream after the dgrad that
@@ -689,10 +703,7 @@ class FFNTrainer:
                     self._side_wait(l, "w2")
                 if self.ddp:
                     self._ddp_wait(l, "w2")
-                xin = self.xs_full[l] if keep else self.xfull
-                comm.all_gather_into(xin, self.xs[l], tpg, async_op=True).wait()
-                layer_fwd(xin, w1, w2, act, gated, a, h, self.yfull, mask=self._mask(l))
-                comm.reduce_scatter_into(self.xs[l + 1], self.yfull, tpg, async_op=True).wait()
+                self._sp_fwd(l, self.xs_full[l] if keep else self.xfull, w1, w2, a, h)
             else:
                 before2 = None
                 if self.zero:
@@ -756,18 +767,20 @@ class FFNTrainer:
             hooks = _Hooks(self, l)
             if self.sp:
                 # gather dy (T-sharded) and the layer input; dx partial -> reduce-scatter
-                comm.all_gather_into(self.dyfull, g, tpg, async_op=True).wait()
+                for w in self._sp_gather(self.dyfull, g):
+                    w.wait()
                 xin = self.xs_full[l] if keep else self.xfull
                 if not keep:
-                    comm.all_gather_into(xin, self.xs[l], tpg, async_op=True).wait()
+                    for w in self._sp_gather(xin, self.xs[l]):
+                        w.wait()
                     recompute_fwd1(xin, w1, act, gated, a, h, mask=self._mask(l))
                 hooks_sp = _SPHooks(self, l)
                 dxp = layer_bwd(self.dyfull, xin, w1, w2, act, gated, a, h, gw1, gw2, self.da,
                                 self.dxb[l % 2] if need_dx else None, hooks_sp, mask=self._mask(l),
                                 dx_first=cfg.tp_overlap)
                 if dxp is not None:
-                    if hooks_sp.rs_work is not None:
-                        hooks_sp.rs_work.wait()
+                    for w in hooks_sp.rs_work or ():
+                        w.wait()
                     g = self.dxs[l % 2]
             elif self.wg_stream is not None:
                 g = self._layer_bwd_concurrent(l, g, w1, w2, a, h, gw1, gw2, need_dx)
@@ -821,6 +834,47 @@ class FFNTrainer:
         if cfg.debug_sync:
             self.check_health()
         return y
+
+    def _sp_parts(self, full: torch.Tensor, local: torch.Tensor) -> list:
+        """(chunk of the gathered [T, *] buffer, this rank's matching sub-slice of its T/tp rows) per SP chunk."""
+        c = self.sp_chunks
+        rf, rl = self.T // c, self.Tl // c
+        return [(full[i * rf:(i + 1) * rf], local[i * rl:(i + 1) * rl]) for i in range(c)]
+
+    def _sp_gather(self, full: torch.Tensor, local: torch.Tensor) -> list:
+        """Async all-gather of every rank's T/tp rows into ``full`` in the chunk-major order (one per chunk)."""
+        tpg = self.mesh.group("tp")
+        return [comm.all_gather_into(f, lo, tpg, async_op=True) for f, lo in self._sp_parts(full, local)]
+
+    def _sp_scatter(self, local: torch.Tensor, full: torch.Tensor) -> list:
+        """Async reduce-scatter of a chunk-major partial ``full`` into this rank's T/tp rows (one per chunk)."""
+        tpg = self.mesh.group("tp")
+        return [comm.reduce_scatter_into(lo, f, tpg, async_op=True) for f, lo in self._sp_parts(full, local)]
+
+    def _sp_fwd(self, l: int, xin: torch.Tensor, w1, w2, a, h) -> None:
+        """Sequence-parallel forward of layer l in ``sp_chunks`` chunks: every chunk's input gather is issued up
+        front (chunk i+1's runs under chunk i's GEMMs), chunk i's partial output is reduce-scattered as soon as
+        its GEMMs are done (under chunk i+1's).  The next layer's gathers queue behind these reduce-scatters on
+        the TP communicator; the last layer's are waited at the end of the forward.  (Reference TP: synchronous
+        all_reduce of y, train_ffns.py:300-303.)"""
+        c = self.sp_chunks
+        rf = self.T // c
+        mask = self._mask(l)
+        mband = (rf // 256) * (self.F_loc // 256) * 8192 if mask is not None else 0  # mask bytes per chunk
+        # the previous layer's reduce-scatters wrote xs[l]: on RCCL they precede these gathers on the TP stream
+        # anyway (the waits are stream waits); gloo may run queued collectives concurrently
+        for w in self._tp_pending or ():
+            w.wait()
+        gathers = self._sp_gather(xin, self.xs[l])
+        tpg = self.mesh.group("tp")
+        pend = []
+        for i, (yf, yl) in enumerate(self._sp_parts(self.yfull, self.xs[l + 1])):
+            gathers[i].wait()
+            r = slice(i * rf, (i + 1) * rf)
+            layer_fwd(xin[r], w1, w2, self.act, self.gated, a[r], h[r] if h is not None else None, yf,
+                      mask=mask[i * mband:(i + 1) * mband] if mask is not None else None)
+            pend.append(comm.reduce_scatter_into(yl, yf, tpg, async_op=True))
+        self._tp_pending = pend
 
     def _tp_fwd_chunked(self, l: int, w1, w2, a, h, before2) -> None:
         """Tensor-parallel forward of layer l in ``tp_chunks`` row chunks: chunk i's partial-output all-reduce
@@ -896,9 +950,10 @@ class _SPHooks(_Hooks):
 
     def after_dx(self, dx):
         e = self.eng
-        self.rs_work = comm.reduce_scatter_into(e.dxs[self.layer % 2], dx, e.mesh.group("tp"), async_op=True)
+        self.rs_work = e._sp_scatter(e.dxs[self.layer % 2], dx)
         if not e.cfg.tp_overlap:
-            self.rs_work.wait()
+            for w in self.rs_work:
+                w.wait()
             self.rs_work = None
 
     def after_w1(self):

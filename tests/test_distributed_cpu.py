@@ -246,6 +246,15 @@ def test_sequence_parallel_async_dx(free_port):
     _close(_run(cfg, 4, 2, free_port), _oracle(cfg, 1))
 
 
+@pytest.mark.parametrize("recompute", ["none", "full"])
+def test_sequence_parallel_chunked_forward(recompute, free_port):
+    """SP forward in 4 chunks (chunk i+1's input gather and chunk i's output reduce-scatter under chunk i's
+    GEMMs; gathered buffers in a chunk-major row order, used consistently by the backward's dy / input gathers
+    and dx reduce-scatters) trains like the single device -- with kept activations and with recompute."""
+    cfg = _cfg(D=32, F=64, L=3, T=1024, steps=2, sequence_parallel=True, tp_chunks=4, recompute=recompute)
+    _close(_run(cfg, 4, 2, free_port), _oracle(cfg, 1))
+
+
 def _update_err(got, want, init) -> float:
     worst = 0.0
     for g, w, i in zip(got, want, init):
