@@ -293,8 +293,16 @@ def main(argv=None) -> int:
         if m == "tp":
             mm = ModelConfig(model_size=a.model_size, ffn_dim=a.mp_ffn_dim, layers=a.mp_layers, act=a.act,
                              gated=a.gated)
-        r = run_method(a, m, n, world, dev, a.method_steps or min(a.steps, 10), min(a.warmup, 3),
-                       force_comm=(world == 1), model=mm, observe_steps=a.observe_steps)
+        try:
+            r = run_method(a, m, n, world, dev, a.method_steps or min(a.steps, 10), min(a.warmup, 3),
+                           force_comm=(world == 1), model=mm, observe_steps=a.observe_steps)
+        except (ValueError, RuntimeError) as e:
+            # a side measurement must not cost the headline line (a config / memory error raises on every
+            # rank alike); a hung collective is not recoverable here either way
+            side[m] = {"error": f"{type(e).__name__}: {e}"[:300]}
+            if not cpu:
+                torch.cuda.empty_cache()
+            continue
         side[m] = {k: r[k] for k in SIDE_KEYS if k in r}
 
     rec = {

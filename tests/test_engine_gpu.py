@@ -65,6 +65,42 @@ def test_bf16_engine_matches_mixed_precision_oracle(act):
             assert rel < (6e-2 if act == "relu" else 2e-2), (k, rel.item())
 
 
+@pytest.mark.parametrize("relu_mask", [True, False])
+def test_bf16_relu_stack_teacher_forced(relu_mask):
+    """Tight stack-level check of the bf16 ReLU path (the 6 % above is mask flips, not kernel error): the oracle
+    backward runs on the engine's OWN stored forward activations (same bf16 values -> same ReLU masks), so what
+    is left is accumulation order and the bf16 rounding of da / dx.  Also each layer's stored output against
+    a_l . W2^T of the engine's a_l.  One step, 3 layers, fp32 master / fp32 gradients."""
+    D, F, L, T, lr = 256, 1024, 3, 512, 1e-2
+    layers, batches = _setup(D, F, L, T, "relu", False, 1)
+    cfg = TrainConfig(model=ModelConfig(D, F, L, "relu", False), batch_size=1, seq_len=T, dtype="bf16",
+                      grad_dtype="fp32", lr=lr, skip_input_grad=False, relu_mask=relu_mask)
+    eng = FFNTrainer(cfg, Mesh(), torch.device("cuda"))
+    assert (eng.masks is not None) == relu_mask
+    eng.load_full_params(layers)
+    x, dy = (t.cuda().bfloat16() for t in batches[0])
+    eng.train_step(x, dy)
+    torch.cuda.synchronize()
+    got = eng.gather_full_params()
+    W = [{k: v.cuda().bfloat16().float() for k, v in p.items()} for p in layers]
+    xs = [x.float()] + [eng.xs[l + 1].float() for l in range(L)]
+    As = [eng.acts_a[l].float() for l in range(L)]
+    for l in range(L):
+        assert torch.equal(As[l], torch.relu(As[l]))
+        y = (As[l] @ W[l]["w2"].t()).bfloat16().float()
+        assert ((xs[l + 1] - y).abs() > 1e-2 * y.abs() + 1e-6).float().mean() < 1e-3, l  # <= 1-ulp bf16 rounding
+    g = dy.float()
+    for l in reversed(range(L)):
+        da = ((g @ W[l]["w2"]) * (As[l] > 0)).bfloat16().float()
+        want = {"w2": layers[l]["w2"].cuda() - lr * (g.t() @ As[l]), "w1": layers[l]["w1"].cuda() - lr * (da.t() @ xs[l])}
+        for k in ("w1", "w2"):
+            d_got = got[l][k].cuda().double() - layers[l][k].cuda().double()
+            d_want = want[k].double() - layers[l][k].cuda().double()
+            rel = float((d_got - d_want).norm() / d_want.norm())
+            assert rel < 5e-3, (l, k, rel)
+        g = (da @ W[l]["w1"]).bfloat16().float()
+
+
 def test_bf16_gated_engine_tracks_fp32_oracle():
     D, F, L, T, lr = 256, 1024, 2, 512, 1.0
     layers, batches = _setup(D, F, L, T, "silu", True, 2)
