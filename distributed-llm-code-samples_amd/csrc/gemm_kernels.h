@@ -1571,16 +1571,31 @@ static int num_cu() {
 
 // grid of a persistent 8-phase launch over nb tile slots; sets a.tpb (1: launch the one-tile kernel instead).
 // Persistent grids are a multiple of the 8 XCDs (every slot of a block maps to the block's own XCD).
+// Tiles per block t <= tpb_req, and <= ceil(nb / (ncu * min_bpc)) (blocks enough to leave CUs to collectives), chosen
+// to minimise the makespan in tile-times, ceil(blocks / ncu) * ceil(nb / blocks) (one block per CU: 128 KiB
+// LDS); ties go to fewer blocks.  E.g. 1792 tiles on 256 CUs: 256 blocks x 7 tiles = 7 tile-times, where a
+// fixed 4 per block (448 blocks in two rounds) takes 8.
 static int grid_8ph(GemmArgs& a, int nb) {
   a.tpb = 1;
   const int ncu = num_cu();
   if (a.tpb_req <= 1 || ncu <= 0) return nb;
-  const int t = std::min(a.tpb_req, nb / (ncu * std::max(1, a.min_bpc)));
-  if (t <= 1) return nb;
-  const int g = ((nb + t - 1) / t + 7) / 8 * 8;
-  if (g >= nb) return nb;
-  a.tpb = t;
-  return g;
+  const int per = ncu * std::max(1, a.min_bpc);
+  const int tmax = std::min(a.tpb_req, (nb + per - 1) / per);
+  auto makespan = [&](long g) { return ((g + ncu - 1) / ncu) * ((nb + g - 1) / g); };
+  int best_g = nb;
+  long best = makespan(nb);
+  for (int t = 2; t <= tmax; ++t) {
+    const int g = ((nb + t - 1) / t + 7) / 8 * 8;
+    if (g >= nb) continue;
+    const long m = makespan(g);
+    if (m < best || (m == best && g < best_g)) {
+      best = m;
+      best_g = g;
+    }
+  }
+  if (best_g >= nb) return nb;
+  a.tpb = (nb + best_g - 1) / best_g;
+  return best_g;
 }
 
 // main kernel writes partials into the workspace, then the reduction applies the epilogue

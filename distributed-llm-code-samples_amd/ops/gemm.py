@@ -163,7 +163,7 @@ _VARIANT = {"name": "auto"}
 # Launch policy of the 256x256 bf16 kernels (tiles per persistent block, minimum blocks per CU): Python-level
 # defaults that every call passes to the library explicitly -- the native side keeps no mutable state, so
 # GEMMs issued concurrently on different streams never race on a setting.
-_POLICY = {"tpb": 4, "min_bpc": 1}
+_POLICY = {"tpb": 8, "min_bpc": 1}  # tpb: the cap; the library picks the makespan-optimal tiles per block
 # split-K fp32 partial workspaces, cached per (device, stream): a GEMM only ever reuses its own stream's
 # buffer, so stream order serialises the reuse
 _WS: dict = {}

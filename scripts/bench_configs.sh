@@ -2,7 +2,7 @@
 # All BASELINE.json configs on the GPUs of this box (1 GPU: multi-GPU configs run their per-rank shapes).
 source scripts/gpu_steps.sh
 OUT=gpurun_out/bench_configs.jsonl; : > $OUT
-b() { local name=$1; shift; step "cfg_$name" 900 python bench.py --json_out gpurun_out/cfg_$name.json "$@" && \
+b() { local name=$1; shift; step "cfg_$name" 900 python bench.py --methods none --json_out gpurun_out/cfg_$name.json "$@" && \
       python -c "import json,sys; d=json.load(open('gpurun_out/cfg_$name.json')); d['bench_config']='$name'; print(json.dumps(d))" >> $OUT; }
 b c2_ddp_L8_D4096 --steps 10 --warmup 3 --method ddp
 b c2_zero_L8_D4096 --steps 10 --warmup 3 --method zero

@@ -320,8 +320,9 @@ def test_persistent_blocks_bitwise_equal(tpb, layout, epi):
     bitwise the same results as one block per tile: same tiles, same K order, same epilogue."""
     from dllm.ops.gemm import set_tiles_per_block
 
-    # 561 tiles: >= 2 per CU, so blocks run 2 tiles (288 blocks: 273 with two, 15 with one)
-    M, N, K = 4352, 8448, 384
+    # 1000 tiles: persistent grids with uneven blocks for every cap (tpb 2: 504 blocks, 496 with two tiles and 8
+    # with one; tpb 3 / 64: the makespan-optimal 2 per block, or 4 per block on 256 blocks, 24 of them with 3)
+    M, N, K = 6400, 10240, 384
     a, b = _operands(layout, M, N, K, torch.bfloat16, seed=41)
     a, b = a.cuda(), b.cuda()
     res = []
