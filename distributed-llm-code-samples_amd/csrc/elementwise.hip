@@ -7,6 +7,7 @@
 //                       Replaces param.add_(-LR*grad) (train_ffns.py:172,259,312) / p-LR*g (:114).
 // * dllm_adam_step    : fused AdamW (north-star optimizer), same flat-buffer contract.
 // * dllm_cast         : fp32 <-> bf16.
+// * dllm_split3       : exact three-way bf16 split of an fp32 GEMM operand (the fp32-accurate bf16x6 GEMM).
 // All kernels: grid-stride, 4 elements per lane per iteration (16-B fp32 / 8-B bf16 accesses),
 // grid capped at 256 CUs x 8 blocks (cdna_hip_programming.md Guideline 11).
 #include <algorithm>
@@ -167,6 +168,64 @@ __global__ __launch_bounds__(512) void sgd_stream_kernel(float* master, const vo
   }
 }
 
+// Three-way bf16 split of an fp32 GEMM operand (the fp32-accurate "bf16x6" GEMM, ops/gemm.py).
+// x = x0 + x1 + x2 exactly for finite normal x: x0 = bf16(x), x1 = bf16(x - x0), x2 = bf16(x - x0 - x1), each
+// difference exact in fp32 (24 = 8 + 8 + 8 mantissa bits, RNE giving each part a spare bit).  The GEMM then runs
+// on the bf16 MFMA kernels with K' = 6K: plane p of A' times plane p of B' is one partial product x_i * y_j; the
+// six with i + j <= 2 are kept (the dropped ones are < 2^-24 relative), the smallest accumulated first:
+//   A' planes (a0, a1, a2, a0, a1, a0)  x  B' planes (b2, b1, b0, b1, b0, b0).
+// Products of bf16 values are exact in fp32 and the MFMA accumulates in fp32, so the result carries fp32 GEMM
+// accuracy at bf16 matrix-core rate (2.5 PF / 6 products > the 157 TF fp32 MFMA peak).
+// rows_form 0: src [R, C] with K = C  -> dst [R, 6C],  dst[r, p*C + c]
+// rows_form 1: src [R, C] with K = R  -> dst [6R, C],  dst[p*R + r, c]
+// 8 elements per lane: two 16-B loads, six 16-B stores (C % 8 == 0, 16-B aligned rows).
+__device__ __forceinline__ void split3(float x, uint16_t& h0, uint16_t& h1, uint16_t& h2) {
+  h0 = f2bf(x);
+  if (!__builtin_isfinite(bf2f(h0))) {
+    if (!__builtin_isfinite(x)) {  // inf / nan: carried in x0 alone (no nan from inf - inf)
+      h1 = 0;
+      h2 = 0;
+      return;
+    }
+    h0 = (uint16_t)(__float_as_uint(x) >> 16);  // finite x above the bf16 range: truncate instead of rounding up
+  }
+  const float x0 = bf2f(h0);
+  const float r1 = x - x0;
+  h1 = f2bf(r1);
+  h2 = f2bf(r1 - bf2f(h1));
+}
+
+__global__ __launch_bounds__(256) void split3_kernel(const float* __restrict__ src, long lds, long R, long C,
+                                                     uint16_t* __restrict__ dst, int role, int rows_form) {
+  const long c8 = C / 8, n8 = R * c8;
+  // plane -> which part of x it carries, per role (A: 0,1,2,0,1,0; B: 2,1,0,1,0,0)
+  const int codeA = 0 | (1 << 2) | (2 << 4) | (0 << 6) | (1 << 8) | (0 << 10);
+  const int codeB = 2 | (1 << 2) | (0 << 4) | (1 << 6) | (0 << 8) | (0 << 10);
+  const int code = role == 0 ? codeA : codeB;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / c8, c = (i - r * c8) * 8;
+    const f32x4_t v0 = *(const f32x4_t*)(src + r * lds + c);
+    const f32x4_t v1 = *(const f32x4_t*)(src + r * lds + c + 4);
+    uint16_t h[3][8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      split3(v0[j], h[0][j], h[1][j], h[2][j]);
+      split3(v1[j], h[0][j + 4], h[1][j + 4], h[2][j + 4]);
+    }
+    uint4 w[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      w[q] = make_uint4((uint32_t)h[q][0] | ((uint32_t)h[q][1] << 16), (uint32_t)h[q][2] | ((uint32_t)h[q][3] << 16),
+                        (uint32_t)h[q][4] | ((uint32_t)h[q][5] << 16), (uint32_t)h[q][6] | ((uint32_t)h[q][7] << 16));
+#pragma unroll
+    for (int p = 0; p < 6; ++p) {
+      const int q = (code >> (2 * p)) & 3;
+      const long off = rows_form ? ((long)p * R + r) * C + c : r * 6 * C + (long)p * C + c;
+      *(uint4*)(dst + off) = w[q];
+    }
+  }
+}
+
 static inline int grid_for(long n4) {
   long g = (n4 + 255) / 256;
   if (g > 2048) g = 2048;
@@ -245,6 +304,16 @@ int dllm_cast(const void* in, int in_dtype, void* out, int out_dtype, long n, vo
   return (int)hipGetLastError();
 }
 
-int dllm_abi_version() { return 3; }
+// bf16x6 operand split (see split3_kernel); role 0 = A (left operand), 1 = B
+int dllm_split3(const float* src, long lds, long R, long C, void* dst, int role, int rows_form, void* stream) {
+  if (R <= 0 || C <= 0 || C % 8 || lds % 4 || (uintptr_t)src % 16 || (uintptr_t)dst % 16) return -1;
+  const long n8 = R * (C / 8);
+  int g = (int)std::min<long>((n8 + 255) / 256, 2048);
+  hipLaunchKernelGGL(split3_kernel, dim3(g), dim3(256), 0, (hipStream_t)stream, src, lds, R, C, (uint16_t*)dst,
+                     role, rows_form);
+  return (int)hipGetLastError();
+}
+
+int dllm_abi_version() { return 4; }
 
 }  // extern "C"

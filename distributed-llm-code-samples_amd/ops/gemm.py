@@ -33,7 +33,7 @@ from .activations import act_code, act_fwd, act_grad
 
 LAYOUTS = {"nt": 0, "nn": 1, "tn": 2}
 EPIS = {"store": 0, "act": 1, "dact": 2, "glu": 3, "dglu": 4, "sgd": 5, "adam": 6}
-FORCE = {None: -1, "mfma_bf16": 0, "mfma_f32": 1, "generic": 2}
+FORCE = {None: -1, "mfma_bf16": 0, "mfma_f32": 1, "generic": 2, "bf16x6": -1}
 
 
 def gemm_shape(a: torch.Tensor, b: torch.Tensor, layout: str) -> tuple[int, int, int]:
@@ -119,6 +119,55 @@ def _torch_gemm(a, b, layout, out, epi, act, aux, aux_out, alpha, beta, opt=None
         out.sub_(opt["lr"] * upd)
         if aux_out is not None:
             aux_out.copy_(out)
+    return out
+
+
+# fp32 GEMMs on the GPU: "bf16x6" (default) runs the exact three-way bf16 split on the bf16 MFMA kernels
+# (fp32 accuracy, ~1.7x the fp32 MFMA rate); "mfma_f32" runs the fp32 MFMA kernel (v_mfma_f32_16x16x4_f32)
+_FP32 = {"mode": "bf16x6"}
+FP32_MODES = ("bf16x6", "mfma_f32")
+# split operands, cached per (device, stream, operand): a GEMM only reuses its own stream's buffers
+_SPLIT_WS: dict = {}
+
+
+def set_fp32_mode(mode: str) -> str:
+    """Select how fp32 GEMMs run on the GPU (``FP32_MODES``); returns the previous mode."""
+    if mode not in FP32_MODES:
+        raise ValueError(f"unknown fp32 GEMM mode {mode!r}")
+    old = _FP32["mode"]
+    _FP32["mode"] = mode
+    return old
+
+
+def bf16x6_supported(M: int, N: int, K: int) -> bool:
+    """Shapes the split fp32 GEMM takes: 256x256 output tiles and K' = 6K a multiple of the 128-deep K step."""
+    return M % 256 == 0 and N % 256 == 0 and K % 64 == 0
+
+
+def _use_bf16x6(M: int, N: int, K: int, force) -> bool:
+    if force == "bf16x6":
+        if not bf16x6_supported(M, N, K):
+            raise ValueError(f"bf16x6 fp32 GEMM needs M, N % 256 == 0 and K % 64 == 0, got {(M, N, K)}")
+        return True
+    return force is None and _FP32["mode"] == "bf16x6" and bf16x6_supported(M, N, K)
+
+
+def split3(x: torch.Tensor, role: int, rows_form: bool) -> torch.Tensor:
+    """Three-way bf16 split of an fp32 operand, six planes along its K dimension (``role`` 0 = A, 1 = B).
+
+    ``rows_form`` False: ``x`` is ``[R, K]`` -> ``[R, 6K]``; True: ``x`` is ``[K, C]`` -> ``[6K, C]``.  The planes
+    carry (a0, a1, a2, a0, a1, a0) for A and (b2, b1, b0, b1, b0, b0) for B, so a bf16 GEMM over the 6K axis sums
+    the six partial products a_i b_j with i + j <= 2."""
+    R, C = x.shape
+    n = 6 * R * C
+    key = (x.device.index, torch.cuda.current_stream(x.device).cuda_stream, role)
+    ws = _SPLIT_WS.get(key)
+    if ws is None or ws.numel() < n:
+        ws = torch.empty(n, dtype=torch.bfloat16, device=x.device)
+        _SPLIT_WS[key] = ws
+    out = ws[:n].view(6 * R, C) if rows_form else ws[:n].view(R, 6 * C)
+    _native.check(_native.lib().dllm_split3(x.data_ptr(), x.stride(0), R, C, out.data_ptr(), role, int(rows_form),
+                                            _native.stream_ptr(x.device)), "dllm_split3")
     return out
 
 
@@ -213,6 +262,14 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
 
     for t, nm in ((a, "a"), (b, "b"), (out, "out")):
         _check_rowmajor(t, nm)
+    if (a.dtype == torch.float32 and mask is None and _use_bf16x6(M, N, K, force)
+            and all(t.data_ptr() % 16 == 0 and t.stride(0) % 4 == 0 for t in (a, b))):
+        # fp32-accurate GEMM on the bf16 matrix cores: split both operands into three bf16 parts and run one
+        # bf16 GEMM over K' = 6K with the same fused epilogue (see split3 / csrc/elementwise.hip split3_kernel)
+        a6 = split3(a, 0, layout == "tn")
+        b6 = split3(b, 1, layout != "nt")
+        return gemm(a6, b6, layout, out, epi=epi, act=act, aux=aux, aux_out=aux_out, alpha=alpha, beta=beta,
+                    group_m=group_m, lr=lr, betas=betas, eps=eps, wd=wd, step=step, opt_m=opt_m, opt_v=opt_v)
     auxt = aux if aux is not None else aux_out
     if auxt is not None:
         _check_rowmajor(auxt, "aux")

@@ -126,9 +126,10 @@ class FFNTrainer:
         self.step_count = 0
         dev = self.device
         if dev.type == "cuda":
-            from ..ops.gemm import set_min_blocks_per_cu, set_tiles_per_block
+            from ..ops.gemm import set_fp32_mode, set_min_blocks_per_cu, set_tiles_per_block
 
             set_tiles_per_block(cfg.gemm_tiles_per_block or (1 if m.gated else 8))
+            set_fp32_mode(cfg.fp32_gemm)
             # collectives overlapping the GEMMs (any multi-rank mesh, or forced size-1 communicators)
             set_min_blocks_per_cu(2 if (mesh.world > 1 or cfg.force_comm) else 1)
         if cfg.debug_sync:

@@ -80,6 +80,8 @@ class TrainConfig:
     comm_backend: str = "torch"      # torch (ProcessGroupNCCL/gloo) | native (csrc/comm.cpp RCCL layer)
     tp_allreduce: str = "rccl"       # TP activation all-reduce: rccl (role communicator) | custom (csrc/car.hip)
     debug_sync: bool = False         # race screen: wait every collective at issue + device sync per layer
+    fp32_gemm: str = "bf16x6"        # fp32 compute GEMMs (process-wide): bf16x6 (exact 3-way bf16 split on the
+                                     # bf16 MFMA kernels, fp32 accuracy) | mfma_f32 (fp32 MFMA kernel)
 
     @property
     def tokens(self) -> int:
@@ -135,5 +137,7 @@ def add_extended_args(p: argparse.ArgumentParser) -> None:
     p.add_argument("--metrics_jsonl", default="")
     p.add_argument("--strict", action="store_true", help="exit non-zero when method results disagree")
     p.add_argument("--master_port", type=int, default=29500)
+    p.add_argument("--fp32_gemm", choices=["bf16x6", "mfma_f32"], default="bf16x6",
+                   help="how --dtype fp32 GEMMs run: exact bf16 3-way split on the bf16 matrix cores, or fp32 MFMA")
     p.add_argument("--debug_sync", action="store_true",
                    help="race screen: serialize every collective (must match the overlapped run bitwise)")

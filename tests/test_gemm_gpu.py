@@ -146,9 +146,62 @@ def test_fp32_mfma_exact_f32(layout, M, N, K):
     assert ((out - ref).abs().max() / ref.abs().max()) < 1e-6
 
 
+@pytest.fixture(params=["mfma_f32", "bf16x6"])
+def fp32_mode(request):
+    from dllm.ops.gemm import set_fp32_mode
+
+    old = set_fp32_mode(request.param)
+    yield request.param
+    set_fp32_mode(old)
+
+
+def test_split3_planes_are_exact():
+    """The bf16x6 operand split: the three bf16 parts sum exactly to the fp32 input (normals, wide exponent range,
+    signed zeros), an inf/nan lands in part 0 alone, and the six planes follow the A / B pairing in both forms."""
+    from dllm.ops.gemm import split3
+
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(64, 96, generator=g) * torch.exp2(torch.randint(-60, 60, (64, 96), generator=g).float())
+    x[0, :8] = torch.tensor([0.0, -0.0, 1.0, -1.0, 3.4e38, 1.1754944e-38, float("inf"), float("nan")])
+    xd = x.to(DEV)
+    for role, order in ((0, (0, 1, 2, 0, 1, 0)), (1, (2, 1, 0, 1, 0, 0))):
+        for rows in (False, True):
+            s = split3(xd, role, rows).cpu()
+            planes = s.view(6, 64, 96) if rows else s.view(64, 6, 96).transpose(0, 1)
+            parts = [None] * 3
+            for p, q in enumerate(order):
+                if parts[q] is None:
+                    parts[q] = planes[p].clone()
+                assert torch.equal(planes[p].view(torch.int16), parts[q].view(torch.int16)), (role, rows, p)
+            tot = parts[0].double() + parts[1].double() + parts[2].double()
+            fin = torch.isfinite(x)  # incl. 3.4e38, above the largest finite bf16 (part 0 truncated, not inf)
+            assert torch.equal(tot[fin], x.double()[fin])
+            assert torch.isinf(parts[0][0, 6].float()) and torch.isnan(parts[0][0, 7].float())
+            assert parts[1][0, 6].item() == 0 and parts[2][0, 7].item() == 0
+
+
+@pytest.mark.parametrize("layout", ["nt", "nn", "tn"])
+@pytest.mark.parametrize("M,N,K", [(256, 512, 64), (512, 256, 1024), (768, 512, 4096)])
+def test_bf16x6_fp32_accuracy(layout, M, N, K):
+    """The split fp32 GEMM (bf16 MFMA, six partial products) carries fp32 accuracy: vs an fp64 reference its error
+    is at the fp32 MFMA kernel's level (both sum K fp32 products in an fp32 accumulator)."""
+    a, b = _operands(layout, M, N, K, torch.float32, seed=31)
+    ref = _ref(a, b, layout)
+    split = gemm(a.to(DEV), b.to(DEV), layout, force="bf16x6").cpu().double()
+    f32 = gemm(a.to(DEV), b.to(DEV), layout, force="mfma_f32").cpu().double()
+    scale = ref.abs().max()
+    e_split, e_f32 = (split - ref).abs().max() / scale, (f32 - ref).abs().max() / scale
+    assert e_split < 2e-6, e_split
+    assert e_split < 3 * e_f32 + 1e-7, (e_split, e_f32)
+    # bf16 inputs would be 2-3 orders of magnitude off: the low parts are really used
+    lo = gemm(a.to(DEV).bfloat16(), b.to(DEV).bfloat16(), layout, out_dtype=torch.float32).cpu().double()
+    assert (lo - ref).abs().max() / scale > 100 * e_split
+
+
 @pytest.mark.parametrize("epi", ["act", "dact", "sgd", "adam", "glu", "beta"])
-def test_fp32_256_epilogues(epi):
-    """The 256x256 fp32 kernel's fused epilogues (shared with the bf16 8-phase kernel) vs the torch oracle."""
+def test_fp32_256_epilogues(epi, fp32_mode):
+    """The fp32 GEMMs' fused epilogues vs the torch oracle: the 256x256 fp32 MFMA kernel and the bf16x6 split
+    path (bf16 8-phase kernel with fp32 outputs); the epilogue code is shared with the bf16 kernels."""
     M, N, K = 512, 512, 256
     layout = {"act": "nt", "dact": "nn", "sgd": "tn", "adam": "tn", "glu": "nt", "beta": "nt"}[epi]
     a, b = _operands(layout, M, N, K, torch.float32, seed=13)
