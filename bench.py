@@ -51,7 +51,7 @@ from dllm.parallel.engine import FFNTrainer
 from dllm.parallel.mesh import Mesh, init_distributed
 from dllm.utils.config import ModelConfig, TrainConfig
 from dllm.utils.data import DeviceMockData
-from dllm.utils.metrics import PEAK_TFLOPS, flops_per_step
+from dllm.utils.metrics import flops_per_step, peak_tflops
 
 METRIC = "FFN tokens/sec (whole node) at hidden=4096 for DDP/FSDP/MP, 1/2/4/8 MI355X"
 MP_FFN = 14336  # BASELINE.json config 4: FFN (hidden=4096, ffn=14336) MP column/row split
@@ -115,6 +115,8 @@ def parse(argv=None):
                    help="N=1: weight-gradient GEMMs (fused SGD) on a second stream, concurrent with the dgrads")
     p.add_argument("--no_relu_mask", action="store_true",
                    help="ReLU dgrad reads the bf16 activation instead of the forward's 1-bit mask")
+    p.add_argument("--fp32_gemm", choices=["bf16x6", "mfma_f32"], default="bf16x6",
+                   help="--dtype fp32 GEMMs: exact 3-way bf16 split on the bf16 MFMA kernels, or the fp32 MFMA kernel")
     p.add_argument("--force_comm", action="store_true",
                    help="exercise the RCCL DDP/FSDP path of the headline at N=1 (size-1 communicators)")
     return p.parse_args(argv)
@@ -180,7 +182,7 @@ def run_method(a, method: str, n: int, world: int, dev: torch.device, steps: int
                       bucket_mb=a.bucket_mb, recompute=a.recompute, sequence_parallel=a.sequence_parallel,
                       data="device", force_comm=force_comm, comm_backend=a.comm,
                       side_optimizer=a.side_opt if headline else 0, tp_allreduce=a.tp_allreduce,
-                      relu_mask=not a.no_relu_mask, gemm_tiles_per_block=a.tpb,
+                      relu_mask=not a.no_relu_mask, gemm_tiles_per_block=a.tpb, fp32_gemm=a.fp32_gemm,
                       wgrad_stream=a.wgrad_stream and headline)
     mesh = Mesh.build(dp, tp, force=force_comm, comm_backend="torch" if cpu else a.comm,
                       device=None if cpu else dev)
@@ -314,7 +316,7 @@ def main(argv=None) -> int:
                    "parallelism": head["parallelism"], "optimizer": a.optimizer, "grad_dtype": a.grad_dtype,
                    "master_weights": "fp32"},
         "tflops_per_gpu": head["tflops_per_gpu"],
-        "mfu_dense": round(head["tflops_per_gpu"] / PEAK_TFLOPS[a.dtype], 4),
+        "mfu_dense": round(head["tflops_per_gpu"] / peak_tflops(a.dtype, a.fp32_gemm), 4),
         "peak_hbm_gib": head["peak_hbm_gib"], "state_gib": head["state_gib"], "finite": head["finite"],
         "comm_backend": a.comm, "hip_graph": bool(a.graph), "gemm_variant": a.gemm_variant,
         "tp_allreduce": a.tp_allreduce,

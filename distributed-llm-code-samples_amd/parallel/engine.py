@@ -238,9 +238,18 @@ class FFNTrainer:
                               for _ in range(nA)]
         # TP forward row chunks (see TrainConfig.tp_chunks): whole 256-row tiles per chunk; the ReLU bitmask is
         # written per chunk (tile-native layout, tile rows contiguous), so chunk GEMMs must stay on its kernels
+        # On the GPU a chunk's two GEMMs must still fill the chip without split-K (fp32 partials + a reduction
+        # pass per chunk cost more than the overlap buys), and a one-layer TP stack is not chunked at all: its
+        # only output exchange is the last layer's, which overlaps the backward anyway (see train_step).
         self.tp_chunks = 1
         c = max(1, cfg.tp_chunks)
-        if t > 1 and not self.sp and c > 1 and T % (256 * c) == 0:
+        if dev.type == "cuda" and c > 1:
+            from ..ops.gemm import choose_ksplit
+
+            while c > 1 and (T % c or choose_ksplit(T // c, self.R1, D) > 1
+                             or choose_ksplit(T // c, D, self.F_loc) > 1):
+                c //= 2
+        if t > 1 and not self.sp and c > 1 and T % (256 * c) == 0 and L > 1:
             if self.masks is None:
                 self.tp_chunks = c
             else:
@@ -722,14 +731,19 @@ class FFNTrainer:
                     continue
                 layer_fwd(self.xs[l], w1, w2, act, gated, a, h, self.xs[l + 1], before_fwd2=before2,
                           mask=self._mask(l))
-                if self.tp_car is not None:
-                    self.tp_car.all_reduce(self.xs[l + 1])
-                elif self.mesh.tp > 1:
-                    comm.all_reduce(self.xs[l + 1], tpg, async_op=True).wait()
-        if self._tp_pending is not None:
-            for w in self._tp_pending:
-                w.wait()
-            self._tp_pending = None
+                if self.mesh.tp > 1:
+                    if self.tp_car is not None:
+                        w = self.tp_car.all_reduce_async(self.xs[l + 1])
+                    else:
+                        w = comm.all_reduce(self.xs[l + 1], tpg, async_op=True)
+                    if l == L - 1:
+                        self._tp_pending = [w]
+                    else:
+                        w.wait()
+        # The last layer's TP output exchange (all-reduce / SP reduce-scatter of y) is left in flight: nothing in
+        # the backward reads y (dL/dy is an input), so it runs under the backward GEMMs and is waited at the end
+        # of the step (reference: synchronous all_reduce(y) before the backward, train_ffns.py:300-303).
+        y_pending, self._tp_pending = self._tp_pending, None
         y = self.xs[L]
 
         self._unmark(mark)
@@ -832,6 +846,8 @@ class FFNTrainer:
         elif not self.fused_opt and not self.side_opt:
             self._opt(0, self.total)
         self._unmark(mark)
+        for w in y_pending or ():
+            w.wait()
         if cfg.debug_sync:
             self.check_health()
         return y

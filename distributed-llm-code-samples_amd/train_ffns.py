@@ -24,7 +24,7 @@ import torch
 
 from .parallel.launch import build_params, spawn
 from .utils.config import METHODS, ModelConfig, TrainConfig, add_extended_args, add_reference_args
-from .utils.metrics import PEAK_TFLOPS, jsonl
+from .utils.metrics import jsonl, peak_tflops
 
 FN_NAMES = {1: "train_1gpu", 2: "train_ddp", 3: "train_fsdp", 4: "train_tp", 5: "train_hybrid", 6: "train_zero"}
 
@@ -113,7 +113,7 @@ def main(argv=None) -> int:
             line["steady_step_ms"] = steady
             line["tokens_per_s_steady"] = rec["tokens_per_step_global"] / (steady / 1e3)
             line["tflops_per_rank"] = rec["flops_per_step_rank"] / (steady / 1e3) / 1e12
-            line["mfu_dense"] = line["tflops_per_rank"] / PEAK_TFLOPS.get(cfg.dtype, PEAK_TFLOPS["fp32"])
+            line["mfu_dense"] = line["tflops_per_rank"] / peak_tflops(cfg.dtype, cfg.fp32_gemm)
         if rec.get("peak_hbm_gib"):
             line["peak_hbm_gib_rank0"] = rec["peak_hbm_gib"]
         print("METRICS", line)

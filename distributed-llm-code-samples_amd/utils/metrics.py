@@ -13,6 +13,14 @@ from .config import TrainConfig
 PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}
 
 
+def peak_tflops(dtype: str, fp32_gemm: str = "bf16x6") -> float:
+    """The ceiling the step's GEMMs run against: fp32 on the bf16x6 split path executes six bf16 MFMA products
+    per fp32 multiply-add, so its ceiling is the bf16 peak / 6 (417 TF), not the fp32 MFMA peak."""
+    if dtype == "fp32" and fp32_gemm == "bf16x6":
+        return PEAK_TFLOPS["bf16"] / 6
+    return PEAK_TFLOPS.get(dtype, PEAK_TFLOPS["fp32"])
+
+
 def flops_per_step(cfg: TrainConfig, tp: int = 1, recompute: str = "none", skip_dx0: bool = True) -> int:
     """Executed FLOPs per rank per step.
 
@@ -70,8 +78,8 @@ class StepTimer:
         return (sum(ts) / len(ts) * 1e3) if ts else None
 
 
-def mfu(tflops: float, dtype: str) -> float:
-    return tflops / PEAK_TFLOPS[dtype]
+def mfu(tflops: float, dtype: str, fp32_gemm: str = "bf16x6") -> float:
+    return tflops / peak_tflops(dtype, fp32_gemm)
 
 
 def jsonl(path: str, rec: dict) -> None:
