@@ -35,6 +35,10 @@
 #define DLLM_PRIO_MODE 0
 #endif
 // fp32 path: the 256x256x32 LDS-DMA kernel where shapes allow (1), or always the 128x128 kernel (0)
+#ifndef DLLM_ADAM_PIPE
+#define DLLM_ADAM_PIPE 1  // fused-AdamW epilogue: row groups per batch, the next batch's master / moment loads issued
+                          // before this batch's stores (0 = sequential batches; profiles/r2/epilogue_pipe_experiment_r2.log)
+#endif
 #ifndef DLLM_F32_256
 #define DLLM_F32_256 1
 #endif
@@ -496,6 +500,50 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
 #pragma unroll
         for (int r = 0; r < RB; ++r)
           st_pair_bf16(p.aux_out, (long)DLLM_M(b0 + r) * p.ldaux + DLLM_NB(b0 + r) + pc, W[r][0], W[r][1]);
+      }
+    }
+  } else if constexpr (EPI == EPI_ADAM && DLLM_ADAM_PIPE) {
+    // software-pipelined: batch b+1's master / moment loads are in flight while batch b is updated and stored, so a
+    // wait for batch b's loads never also waits for the previous batch's stores (loads and stores share vmcnt)
+    constexpr int SB = DLLM_ADAM_PIPE;
+    f32x4_t W[2][SB][2], Mm[2][SB][2], Vv[2][SB][2];
+    auto ld = [&](int b, int s) {
+#pragma unroll
+      for (int r = 0; r < SB; ++r)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const long ci = (long)DLLM_M(b * SB + r) * p.ldc + DLLM_N(b * SB + r, nt);
+          W[s][r][nt] = RF::load(Cp, ci);
+          Mm[s][r][nt] = RF::load(p.opt_m, ci);
+          Vv[s][r][nt] = RF::load(p.opt_v, ci);
+        }
+    };
+    ld(0, 0);
+#pragma unroll
+    for (int b = 0; b < 16 / SB; ++b) {
+      if (b + 1 < 16 / SB) ld(b + 1, (b + 1) & 1);
+      const int s = b & 1;
+#pragma unroll
+      for (int r = 0; r < SB; ++r) {
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const f32x4_t gg = DLLM_ACC(b * SB + r, nt);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float g = p.alpha * gg[e];
+            Mm[s][r][nt][e] = p.b1 * Mm[s][r][nt][e] + (1.f - p.b1) * g;
+            Vv[s][r][nt][e] = p.b2 * Vv[s][r][nt][e] + (1.f - p.b2) * g * g;
+            const float mh = Mm[s][r][nt][e] / p.bc1, vh = Vv[s][r][nt][e] / p.bc2;
+            W[s][r][nt][e] = W[s][r][nt][e] - p.lr * (mh / (sqrtf(vh) + p.eps) + p.wd * W[s][r][nt][e]);
+          }
+          const long ci = (long)DLLM_M(b * SB + r) * p.ldc + DLLM_N(b * SB + r, nt);
+          Vec4<float>::store(Cp, ci, W[s][r][nt]);
+          Vec4<float>::store(p.opt_m, ci, Mm[s][r][nt]);
+          Vec4<float>::store(p.opt_v, ci, Vv[s][r][nt]);
+        }
+        if (p.aux_out)
+          st_pair_bf16(p.aux_out, (long)DLLM_M(b * SB + r) * p.ldaux + DLLM_NB(b * SB + r) + pc, W[s][r][0],
+                       W[s][r][1]);
       }
     }
   } else if constexpr (EPI == EPI_ADAM) {
