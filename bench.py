@@ -28,9 +28,11 @@ utils/observe.py, measured on extra steps after the timed ones):
 * ``zero``  as the headline;
 * ``fsdp``  ZeRO-3 row shards, prefetched all-gathers, async reduce-scatter (train_ffns.py:197-287);
 * ``tp``    the MP config of BASELINE.json: hidden 4096, FFN 14336, one layer, column/row split over the
-            N GPUs (train_ffns.py:290-338; every rank sees every token: strong scaling).
+            N GPUs (train_ffns.py:290-338; every rank sees every token: strong scaling);
+* ``hybrid`` BASELINE config 5: the Llama-3-8B-dims FFN stack (hidden 4096, FFN 14336, SwiGLU/SiLU, 32 layers)
+            on an FSDP x TP mesh (TP = min(N, 2) or ``--tp``; 8192 tokens per FSDP rank).
 
-At N=1 the ddp/zero/fsdp/tp entries run their collective code paths over size-1 communicators
+At N=1 the ddp/zero/fsdp/tp/hybrid entries run their collective code paths over size-1 communicators
 (``force_comm``), so each method's own overhead is visible even on one GPU.  Weak scaling for the DP
 methods: every rank processes 8192 tokens per step (global batch = 8·N sequences).
 """
@@ -64,7 +66,7 @@ def parse(argv=None):
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--method", choices=["ddp", "zero", "fsdp", "tp", "hybrid"], default="zero",
                    help="headline method (see module docstring); zero = DDP semantics as ZeRO-2")
-    p.add_argument("--methods", default="ddp,zero,fsdp,tp",
+    p.add_argument("--methods", default="ddp,zero,fsdp,tp,hybrid",
                    help="comma list of methods also timed side by side ('' or 'none' = headline only)")
     p.add_argument("--method_steps", type=int, default=0,
                    help="timed steps per side-by-side method (0 = min(steps, 10))")
@@ -75,6 +77,9 @@ def parse(argv=None):
     p.add_argument("--ffn_dim", type=int, default=0)
     p.add_argument("--mp_ffn_dim", type=int, default=MP_FFN, help="FFN width of the tp (MP) method entry")
     p.add_argument("--mp_layers", type=int, default=1, help="layers of the tp (MP) method entry")
+    p.add_argument("--llama_ffn_dim", type=int, default=14336,
+                   help="FFN width of the hybrid method entry (BASELINE config 5: Llama-3-8B dims, SwiGLU)")
+    p.add_argument("--llama_layers", type=int, default=32, help="layers of the hybrid method entry")
     p.add_argument("--layers", type=int, default=8)
     p.add_argument("--batch_size", type=int, default=8)
     p.add_argument("--seq_len", type=int, default=1024)
@@ -295,6 +300,9 @@ def main(argv=None) -> int:
         if m == "tp":
             mm = ModelConfig(model_size=a.model_size, ffn_dim=a.mp_ffn_dim, layers=a.mp_layers, act=a.act,
                              gated=a.gated)
+        elif m == "hybrid":
+            mm = ModelConfig(model_size=a.model_size, ffn_dim=a.llama_ffn_dim, layers=a.llama_layers, act="silu",
+                             gated=True)
         try:
             r = run_method(a, m, n, world, dev, a.method_steps or min(a.steps, 10), min(a.warmup, 3),
                            force_comm=(world == 1), model=mm, observe_steps=a.observe_steps)
@@ -327,8 +335,9 @@ def main(argv=None) -> int:
     if side:
         rec["methods"] = side
         if world == 1:
-            rec["methods_note"] = ("N=1: ddp/zero/fsdp/tp run their collective code paths over size-1 "
-                                   "communicators; tp is the MP config (hidden 4096, FFN 14336, 1 layer)")
+            rec["methods_note"] = ("N=1: ddp/zero/fsdp/tp/hybrid run their collective code paths over size-1 "
+                                   "communicators; tp is the MP config (hidden 4096, FFN 14336, 1 layer); hybrid "
+                                   "is the Llama-3-8B-dims SwiGLU stack (32 layers) on FSDP x TP")
     if a.force_comm:
         rec["note"] = "force_comm: headline collectives over size-1 RCCL communicators"
     if cpu:

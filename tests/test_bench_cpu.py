@@ -16,7 +16,7 @@ def _run(free_port, *extra):
            "--master-addr", "127.0.0.1", "--master-port", str(free_port), os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--steps", "2", "--warmup", "1", "--backend", "gloo",
            "--model_size", "64", "--layers", "2", "--batch_size", "2", "--seq_len", "16", "--dtype", "fp32",
-           "--mp_ffn_dim", "128", *extra]
+           "--mp_ffn_dim", "128", "--llama_ffn_dim", "128", "--llama_layers", "2", *extra]
     env = dict(os.environ, PYTHONPATH=ROOT)
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
@@ -37,13 +37,14 @@ def test_bench_torchrun_gloo_two_ranks(method, free_port):
 
 
 def test_bench_methods_side_by_side(free_port):
-    """The default run: ZeRO-2 headline plus ddp / zero / fsdp / tp timed side by side on their own engines
-    (the reference's --method 0, train_ffns.py:373-384)."""
+    """The default run: ZeRO-2 headline plus ddp / zero / fsdp / tp / hybrid timed side by side on their own engines
+    (the reference's --method 0, train_ffns.py:373-384; hybrid = BASELINE config 5, FSDP x TP on a SwiGLU stack)."""
     rec = _run(free_port)
     assert rec["config"]["parallelism"] == "dp2-zero2" and rec["config"]["global_batch"] == 4
-    assert set(rec["methods"]) == {"ddp", "zero", "fsdp", "tp"}
+    assert set(rec["methods"]) == {"ddp", "zero", "fsdp", "tp", "hybrid"}
     for name, m in rec["methods"].items():
         assert m["value"] > 0 and m["ms_per_step"] > 0 and m["finite"], name
         assert {"peak_hbm_gib", "parallelism", "model", "state_gib"} <= set(m), name
     assert rec["methods"]["tp"]["parallelism"] == "tp2" and "L1 D64 F128" in rec["methods"]["tp"]["model"]
     assert rec["methods"]["fsdp"]["parallelism"] == "fsdp2"
+    assert rec["methods"]["hybrid"]["parallelism"] == "fsdp1xtp2" and "L2 D64 F128 swiglu-silu" in rec["methods"]["hybrid"]["model"]
