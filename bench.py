@@ -116,6 +116,8 @@ def parse(argv=None):
                    help="bf16 GEMM main-loop schedule (auto = 8-phase staggered when K % 128 == 0)")
     p.add_argument("--tpb", type=int, default=0,
                    help="tiles per persistent 8-phase GEMM block (0 = auto: 2, or 1 for gated stacks; 1 = off)")
+    p.add_argument("--min_bpc", type=int, default=0,
+                   help="minimum blocks per CU of persistent GEMM grids (0 = auto: 2 with overlapping collectives)")
     p.add_argument("--wgrad_stream", action="store_true",
                    help="N=1: weight-gradient GEMMs (fused SGD) on a second stream, concurrent with the dgrads")
     p.add_argument("--no_relu_mask", action="store_true",
@@ -188,6 +190,7 @@ def run_method(a, method: str, n: int, world: int, dev: torch.device, steps: int
                       data="device", force_comm=force_comm, comm_backend=a.comm,
                       side_optimizer=a.side_opt if headline else 0, tp_allreduce=a.tp_allreduce,
                       relu_mask=not a.no_relu_mask, gemm_tiles_per_block=a.tpb, fp32_gemm=a.fp32_gemm,
+                      gemm_min_bpc=a.min_bpc,
                       wgrad_stream=a.wgrad_stream and headline)
     mesh = Mesh.build(dp, tp, force=force_comm, comm_backend="torch" if cpu else a.comm,
                       device=None if cpu else dev)

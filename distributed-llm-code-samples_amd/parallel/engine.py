@@ -131,7 +131,7 @@ class FFNTrainer:
             set_tiles_per_block(cfg.gemm_tiles_per_block or (1 if m.gated else 8))
             set_fp32_mode(cfg.fp32_gemm)
             # collectives overlapping the GEMMs (any multi-rank mesh, or forced size-1 communicators)
-            set_min_blocks_per_cu(2 if (mesh.world > 1 or cfg.force_comm) else 1)
+            set_min_blocks_per_cu(cfg.gemm_min_bpc or (2 if (mesh.world > 1 or cfg.force_comm) else 1))
         if cfg.debug_sync:
             comm.set_serialize(True)
         # custom xGMI all-reduce for the TP activation exchange (opt-in; gradients stay on RCCL)

@@ -71,6 +71,8 @@ class TrainConfig:
                                      # GEMM instead of the bf16 activation (GPU, 8-phase kernel shapes)
     wgrad_stream: bool = False       # single device, fused optimizer: weight-gradient GEMMs on a second
                                      # stream, concurrent with the dgrad chain (CUs shared; epilogues overlap)
+    gemm_min_bpc: int = 0            # persistent GEMM grids: minimum blocks per CU (0 = auto: 2 when collectives
+                                     # overlap the GEMMs, else 1)
     gemm_tiles_per_block: int = 0    # persistent 8-phase GEMM blocks (process-wide): tiles per block; 0 = auto
                                      # (2 for plain FFN stacks, 1 for gated stacks, where it measured slower)
     fused_optimizer: bool = True     # fuse SGD/Adam into the wgrad GEMM epilogue when no grad collective
