@@ -20,8 +20,10 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
   const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    const uint32_t lo0 = M0 * c.x, hi0 = __umulhi(M0, c.x);
-    const uint32_t lo1 = M1 * c.z, hi1 = __umulhi(M1, c.z);
+    // one 32x32->64 multiply per product (v_mad_u64_u32) instead of separate mul_lo / mul_hi
+    const uint64_t p0 = (uint64_t)M0 * c.x, p1 = (uint64_t)M1 * c.z;
+    const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+    const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
     c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
     k.x += W0;
     k.y += W1;
@@ -32,7 +34,7 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
 __device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, float& z0, float& z1) {
   const float u1 = ((float)a + 1.0f) * 2.3283064365386963e-10f;  // (0, 1]
   const float u2 = (float)b * 2.3283064365386963e-10f;           // [0, 1)
-  const float r = sqrtf(-2.0f * __logf(u1));
+  const float r = __builtin_amdgcn_sqrtf(-2.0f * __logf(u1));  // v_sqrt_f32 (1 ulp; no IEEE fix-up sequence)
   float s, c;
   __sincosf(6.283185307179586f * u2, &s, &c);
   z0 = r * c;
