@@ -94,6 +94,17 @@ class _Hooks:
             self.tp_work = None
 
 
+def gpu_chunk_count(T: int, D: int, F_loc: int, R1: int, c: int) -> int:
+    """Largest chunk count <= ``c`` (halving) whose per-chunk forward GEMMs, ``[T/c, R1]`` (K = D) and ``[T/c, D]``
+    (K = F_loc), need no split-K on the 256x256 kernels, i.e. still fill the chip on their own."""
+    from ..ops.gemm import choose_ksplit
+
+    c = max(1, c)
+    while c > 1 and (T % c or choose_ksplit(T // c, R1, D) > 1 or choose_ksplit(T // c, D, F_loc) > 1):
+        c //= 2
+    return c
+
+
 class FFNTrainer:
     def __init__(self, cfg: TrainConfig, mesh: Mesh, device: torch.device):
         self.cfg, self.mesh, self.device = cfg, mesh, torch.device(device)
@@ -243,12 +254,8 @@ class FFNTrainer:
         # only output exchange is the last layer's, which overlaps the backward anyway (see train_step).
         self.tp_chunks = 1
         c = max(1, cfg.tp_chunks)
-        if dev.type == "cuda" and c > 1:
-            from ..ops.gemm import choose_ksplit
-
-            while c > 1 and (T % c or choose_ksplit(T // c, self.R1, D) > 1
-                             or choose_ksplit(T // c, D, self.F_loc) > 1):
-                c //= 2
+        if dev.type == "cuda":
+            c = gpu_chunk_count(T, D, self.F_loc, self.R1, c)
         if t > 1 and not self.sp and c > 1 and T % (256 * c) == 0 and L > 1:
             if self.masks is None:
                 self.tp_chunks = c

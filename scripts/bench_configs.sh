@@ -6,6 +6,7 @@ b() { local name=$1; shift; step "cfg_$name" 900 python bench.py --methods none 
       python -c "import json,sys; d=json.load(open('gpurun_out/cfg_$name.json')); d['bench_config']='$name'; print(json.dumps(d))" >> $OUT; }
 b c2_ddp_L8_D4096 --steps 10 --warmup 3 --method ddp
 b c2_zero_L8_D4096 --steps 10 --warmup 3 --method zero
+b c2_fp32_reference_dtype_L8_D4096 --steps 5 --warmup 2 --dtype fp32 --grad_dtype fp32
 b c3_fsdp_L8_D4096_forcecomm --steps 10 --warmup 3 --method fsdp --force_comm
 b c4_tp_F14336_L1_full --steps 20 --warmup 5 --method tp --ffn_dim 14336 --layers 1
 b c4_tp8_rank_shard_F1792 --steps 20 --warmup 5 --method tp --ffn_dim 1792 --layers 1

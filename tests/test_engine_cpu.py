@@ -90,3 +90,17 @@ def test_sizing_plan_matches_engine_buffers(gated, act, opt, rec):
     assert p["activations"] == sum(nb(t) for t in eng.acts_a)
     assert p.get("preactivations", 0) == (sum(nb(t) for t in eng.acts_h) if eng.acts_h else 0)
     assert p["dgrad_buffer"] == nb(eng.da) and p["dx_buffers"] == sum(nb(t) for t in eng.dxb)
+
+
+def test_tp_chunk_policy_avoids_split_k_chunks():
+    """TP/SP forward chunks on the GPU: halve the chunk count until each chunk's GEMMs fill the chip without
+    split-K (MP config T=8192, D=4096, F=14336: TP8 shard unchunked, TP2 / TP4 in 2 chunks)."""
+    from dllm.parallel.engine import gpu_chunk_count
+
+    T, D = 8192, 4096
+    assert gpu_chunk_count(T, D, 14336 // 8, 14336 // 8, 4) == 1
+    assert gpu_chunk_count(T, D, 14336 // 4, 14336 // 4, 4) == 2
+    assert gpu_chunk_count(T, D, 14336 // 2, 14336 // 2, 4) == 2
+    assert gpu_chunk_count(T, D, 14336 // 2, 14336, 4) == 2       # gated: R1 = 2 F_loc
+    assert gpu_chunk_count(4 * T, D, 16384 // 2, 16384 // 2, 4) == 4
+    assert gpu_chunk_count(T, D, 8192, 8192, 1) == 1
