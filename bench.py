@@ -43,6 +43,7 @@ import gc
 import json
 import os
 import sys
+import threading
 import time
 
 import torch
@@ -70,6 +71,9 @@ def parse(argv=None):
                    help="comma list of methods also timed side by side ('' or 'none' = headline only)")
     p.add_argument("--method_steps", type=int, default=0,
                    help="timed steps per side-by-side method (0 = min(steps, 10))")
+    p.add_argument("--side_deadline_s", type=float, default=420.0,
+                   help="wall-clock budget of the side-by-side methods after the headline (0 = none): past it, rank 0 "
+                        "prints the line with the methods finished so far and every rank exits")
     p.add_argument("--observe_steps", type=int, default=2,
                    help="extra steps per communicating method under the comm observer (0 = off)")
     p.add_argument("--tp", type=int, default=0, help="TP degree for --method hybrid")
@@ -297,8 +301,73 @@ def main(argv=None) -> int:
     head = run_method(a, a.method, n, world, dev, a.steps, a.warmup, a.force_comm, model,
                       observe_steps=a.observe_steps, headline=True)
 
-    side = {}
+    side: dict = {}
+
+    def record(note: str = "") -> dict:
+        rec = {
+            "metric": METRIC, "value": head["value"], "unit": "tokens/s", "n_gpus": 0 if cpu else n,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": head["ms_per_step"], "higher_is_better": True,
+            "scaling": "strong" if a.method == "tp" else "weak", "vs_baseline": None, "dtype": a.dtype,
+            "data": "synthetic (device Philox N(0,1) x, 0.1*N(0,1) dloss/dx; random-init weights)",
+            "config": {"model": head["model"], "global_batch": head["global_batch"], "seq_len": a.seq_len,
+                       "parallelism": head["parallelism"], "optimizer": a.optimizer, "grad_dtype": a.grad_dtype,
+                       "master_weights": "fp32"},
+            "tflops_per_gpu": head["tflops_per_gpu"],
+            "mfu_dense": round(head["tflops_per_gpu"] / peak_tflops(a.dtype, a.fp32_gemm), 4),
+            "peak_hbm_gib": head["peak_hbm_gib"], "state_gib": head["state_gib"], "finite": head["finite"],
+            "comm_backend": a.comm, "hip_graph": bool(a.graph), "gemm_variant": a.gemm_variant,
+            "tp_allreduce": a.tp_allreduce,
+        }
+        for k in ("comm", "phase_ms_per_step"):
+            if k in head:
+                rec[k] = head[k]
+        if side:
+            rec["methods"] = dict(side)
+            if world == 1:
+                rec["methods_note"] = ("N=1: ddp/zero/fsdp/tp/hybrid run their collective code paths over size-1 "
+                                       "communicators; tp is the MP config (hidden 4096, FFN 14336, 1 layer); "
+                                       "hybrid is the Llama-3-8B-dims SwiGLU stack (32 layers) on FSDP x TP")
+        if a.force_comm:
+            rec["note"] = "force_comm: headline collectives over size-1 RCCL communicators"
+        if cpu:
+            rec["note"] = f"CPU/gloo dry run with {world} ranks (plumbing only, not a measurement)"
+        if note:
+            rec["note"] = (rec.get("note", "") + "; " + note).lstrip("; ")
+        return rec
+
+    printed = threading.Lock()
+    done = {"printed": False}
+
+    def emit(rec: dict) -> None:
+        with printed:
+            if done["printed"]:
+                return
+            done["printed"] = True
+            if rank == 0:
+                print(json.dumps(rec), flush=True)
+                if a.json_out:
+                    with open(a.json_out, "w") as f:
+                        json.dump(rec, f)
+
+    # The headline is measured; the side-by-side methods must not be able to lose it.  A side method that hangs
+    # (e.g. a collective that never completes) is cut off at the deadline on every rank: rank 0 prints the line
+    # with the methods finished so far, and each rank exits cleanly instead of waiting for the launcher's kill.
+    current = {"m": None}
+
+    def on_deadline() -> None:
+        if not done["printed"]:
+            side[current["m"] or "?"] = {"error": f"not finished within --side_deadline_s {a.side_deadline_s}"}
+            emit(record(f"side method {current['m']} cut off at the deadline"))
+        sys.stdout.flush()
+        os._exit(0)
+
+    watchdog = None
+    if methods and a.side_deadline_s > 0:
+        watchdog = threading.Timer(a.side_deadline_s, on_deadline)
+        watchdog.daemon = True
+        watchdog.start()
     for m in methods:
+        current["m"] = m
         mm = model
         if m == "tp":
             mm = ModelConfig(model_size=a.model_size, ffn_dim=a.mp_ffn_dim, layers=a.mp_layers, act=a.act,
@@ -311,45 +380,14 @@ def main(argv=None) -> int:
                            force_comm=(world == 1), model=mm, observe_steps=a.observe_steps)
         except (ValueError, RuntimeError) as e:
             # a side measurement must not cost the headline line (a config / memory error raises on every
-            # rank alike); a hung collective is not recoverable here either way
+            # rank alike; a hang is cut off by the deadline above)
             side[m] = {"error": f"{type(e).__name__}: {e}"[:300]}
             if not cpu:
                 torch.cuda.empty_cache()
             continue
         side[m] = {k: r[k] for k in SIDE_KEYS if k in r}
-
-    rec = {
-        "metric": METRIC, "value": head["value"], "unit": "tokens/s", "n_gpus": 0 if cpu else n, "steps": a.steps,
-        "warmup": a.warmup, "ms_per_step": head["ms_per_step"], "higher_is_better": True,
-        "scaling": "strong" if a.method == "tp" else "weak", "vs_baseline": None, "dtype": a.dtype,
-        "data": "synthetic (device Philox N(0,1) x, 0.1*N(0,1) dloss/dx; random-init weights)",
-        "config": {"model": head["model"], "global_batch": head["global_batch"], "seq_len": a.seq_len,
-                   "parallelism": head["parallelism"], "optimizer": a.optimizer, "grad_dtype": a.grad_dtype,
-                   "master_weights": "fp32"},
-        "tflops_per_gpu": head["tflops_per_gpu"],
-        "mfu_dense": round(head["tflops_per_gpu"] / peak_tflops(a.dtype, a.fp32_gemm), 4),
-        "peak_hbm_gib": head["peak_hbm_gib"], "state_gib": head["state_gib"], "finite": head["finite"],
-        "comm_backend": a.comm, "hip_graph": bool(a.graph), "gemm_variant": a.gemm_variant,
-        "tp_allreduce": a.tp_allreduce,
-    }
-    for k in ("comm", "phase_ms_per_step"):
-        if k in head:
-            rec[k] = head[k]
-    if side:
-        rec["methods"] = side
-        if world == 1:
-            rec["methods_note"] = ("N=1: ddp/zero/fsdp/tp/hybrid run their collective code paths over size-1 "
-                                   "communicators; tp is the MP config (hidden 4096, FFN 14336, 1 layer); hybrid "
-                                   "is the Llama-3-8B-dims SwiGLU stack (32 layers) on FSDP x TP")
-    if a.force_comm:
-        rec["note"] = "force_comm: headline collectives over size-1 RCCL communicators"
-    if cpu:
-        rec["note"] = f"CPU/gloo dry run with {world} ranks (plumbing only, not a measurement)"
-    if rank == 0:
-        print(json.dumps(rec), flush=True)
-        if a.json_out:
-            with open(a.json_out, "w") as f:
-                json.dump(rec, f)
+    current["m"] = None
+    emit(record())
     import torch.distributed as dist
 
     if dist.is_initialized():

@@ -48,3 +48,11 @@ def test_bench_methods_side_by_side(free_port):
     assert rec["methods"]["tp"]["parallelism"] == "tp2" and "L1 D64 F128" in rec["methods"]["tp"]["model"]
     assert rec["methods"]["fsdp"]["parallelism"] == "fsdp2"
     assert rec["methods"]["hybrid"]["parallelism"] == "fsdp1xtp2" and "L2 D64 F128 swiglu-silu" in rec["methods"]["hybrid"]["model"]
+
+
+def test_bench_side_methods_deadline_keeps_headline(free_port):
+    """A side-by-side method that overruns --side_deadline_s cannot cost the headline: rank 0 still prints the one
+    line (methods finished so far plus the cut-off one as an error) and every rank exits 0."""
+    rec = _run(free_port, "--side_deadline_s", "0.05")
+    assert "cut off" in rec["note"]
+    assert any("error" in m for m in rec["methods"].values())
