@@ -25,10 +25,25 @@ def pytest_collection_modifyitems(config, items):
             it.add_marker(skip)
 
 
-_PORT = [29700 + (os.getpid() % 500) * 40]
+_PORT = [20000 + (os.getpid() % 400) * 100]
+
+
+def _bindable(port: int) -> bool:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        try:
+            s.bind(("127.0.0.1", port))
+            return True
+        except OSError:
+            return False
 
 
 @pytest.fixture
 def free_port():
-    _PORT[0] += 1
-    return _PORT[0]
+    """A rendezvous port whose next 9 ports are free too (tests use free_port + k for follow-up runs); every
+    test gets its own block of 10, so no test reuses a port another one left in TIME_WAIT."""
+    while True:
+        _PORT[0] += 10
+        if all(_bindable(_PORT[0] + k) for k in range(10)):
+            return _PORT[0]
