@@ -29,7 +29,7 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
   a.ksplit = 1;
   a.tpb = 1;
   a.mask = nullptr;
-  a.variant = variant < 0 || variant > 4 ? 0 : variant;
+  a.variant = variant < 0 || variant > 5 ? 0 : variant;
   a.tpb_req = tpb;
   a.min_bpc = min_bpc < 1 ? 1 : min_bpc;
   a.ws = nullptr;
@@ -66,7 +66,7 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
   if (mask != nullptr) {
     // the bitmask lives in the 8-phase kernels' tile-native layout: both GEMMs of a pair must run them
     if ((epi != EPI_ACT && epi != EPI_DACT) || act != ACT_RELU || in_dtype != DT_BF16 || out_dtype != DT_BF16 ||
-        path != 0 || a.ksplit != 1 || K % (2 * BT_K) != 0 || a.variant == 1)
+        path != 0 || a.ksplit != 1 || (K % (2 * BT_K) != 0 && a.variant != 5) || a.variant == 1)
       return -2;
     a.mask = mask;
   }

@@ -254,11 +254,15 @@ __device__ __forceinline__ void unpair_bf16(uint4 v, f32x4_t& a, f32x4_t& b) {
   b = Raw4<uint16_t>::cvt(uint2{u.z, u.w});
 }
 
-// acc[QM][QN][mt][nt]: lane holds C[m0 + QM*128 + wr*64 + mt*16 + (lane&15)][n0 + QN*128 + wc*32 + nt*16 + 4*(lane>>4) + 0..3]
-// row group rg = QM*8 + QN*4 + mt (16 per wave), 2 column groups (nt) each.
-template <int EPI, typename OutT, int ACT>
+// acc[QM][QN][mt][nt]: lane holds C[m0 + QM*128 + wr*64 + mt*16 + (lane&15)][n0 + QN*QNS + wc*32 + nt*16 + 4*(lane>>4) + 0..3]
+// row group rg = QM*8 + QN*4 + mt (16 per wave), 2 column groups (nt) each.  QNS = quadrant width: 128 for the
+// 256x256 tile (8 waves, wc 0..3), 64 for the 256x128 tile of gemm_bf16_pp (4 waves, wc 0..1).
+template <int EPI, typename OutT, int ACT, int QNS = 128>
 __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2][2][4][2], int m0, int n0,
                                              int wr, int wc, int lane, void* Cp) {
+  constexpr int NWC = QNS / 32;       // waves per tile row
+  constexpr int TW = 2 * QNS;         // tile width
+  constexpr int MASK_WAVES = 2 * NWC; // waves per tile: the ReLU mask holds 16 B per lane and wave
   constexpr bool BF = std::is_same<OutT, uint16_t>::value;
   using R = Raw4<OutT>;
   using RT = typename std::conditional<BF, uint4, f32x4_t>::type;  // bf16: one paired 16-B load per row group
@@ -271,7 +275,7 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
   constexpr int RB = epi_batch(COST);
   const int pc = pair_col(lane);
 #define DLLM_M(rg) (m0 + ((rg) >> 3) * 128 + wr * 64 + ((rg) & 3) * 16 + (lane & 15))
-#define DLLM_NB(rg) (n0 + (((rg) >> 2) & 1) * 128 + wc * 32)
+#define DLLM_NB(rg) (n0 + (((rg) >> 2) & 1) * QNS + wc * 32)
 #define DLLM_N(rg, nt) (DLLM_NB(rg) + (nt) * 16 + 4 * (lane >> 4))
 #define DLLM_ACC(rg, nt) acc[(rg) >> 3][((rg) >> 2) & 1][(rg) & 3][nt]
   // store the row group's two fragments (already epilogue-transformed) to a [*, ld] OutT matrix
@@ -326,8 +330,8 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
       // optional mask: bit rg*8 + nt*4 + e of this thread's 128 = (stored bf16 activation != 0), i.e. exactly
       // the act'(h) the unmasked dgrad derives from the stored activation; one dword per 4 row groups
       const bool mk = p.mask != nullptr;
-      const long tile = (long)(m0 / 256) * (p.N / 256) + n0 / 256;  // 256x256 tiles
-      uint32_t* mw = (uint32_t*)p.mask + (tile * 512 + (wr * 4 + wc) * 64 + lane) * 4;
+      const long tile = (long)(m0 / 256) * (p.N / TW) + n0 / TW;  // 256 x TW tiles
+      uint32_t* mw = (uint32_t*)p.mask + (tile * (MASK_WAVES * 64) + (wr * NWC + wc) * 64 + lane) * 4;
       uint32_t w = 0u;
 #pragma unroll
       for (int rg = 0; rg < 16; ++rg) {
@@ -366,8 +370,8 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
   } else if constexpr (EPI == EPI_DACT) {
     if constexpr (ACT == ACT_RELU && BF) {
       if (p.mask) {
-        const long tile = (long)(m0 / 256) * (p.N / 256) + n0 / 256;  // 256x256 tiles
-        const uint4 mv = ((const uint4*)p.mask)[tile * 512 + (wr * 4 + wc) * 64 + lane];
+        const long tile = (long)(m0 / 256) * (p.N / TW) + n0 / TW;  // 256 x TW tiles
+        const uint4 mv = ((const uint4*)p.mask)[tile * (MASK_WAVES * 64) + (wr * NWC + wc) * 64 + lane];
         const uint32_t w[4] = {mv.x, mv.y, mv.z, mv.w};
 #pragma unroll
         for (int rg = 0; rg < 16; ++rg) {
@@ -1603,6 +1607,8 @@ __global__ __launch_bounds__(256) void splitk_reduce(GemmArgs p, const float* ws
   }
 }
 
+#include "gemm_pp.h"
+
 constexpr int MAX_DEV = 64;
 inline int g_num_cu[MAX_DEV] = {};
 
@@ -1646,6 +1652,67 @@ static int grid_8ph(GemmArgs& a, int nb) {
   return best_g;
 }
 
+// grid of a persistent 256x128 (gemm_bf16_pp) launch over nb tile slots: two blocks per CU (80 KiB LDS each), so the
+// makespan in tile-times is ceil(blocks / (2 ncu)) * ceil(nb / blocks); at least max(2, min_bpc) blocks per CU.  Sets
+// a.tpb (1: one block per tile).  A slot needs >= 2 K-tiles for the cross-slot prefetch (K-tiles nk, nk+1 = the next
+// slot's 0, 1).
+static int grid_pp(GemmArgs& a, int nb, int nk) {
+  a.tpb = 1;
+  const int ncu = num_cu();
+  if (a.tpb_req <= 1 || ncu <= 0 || nk < 2) return nb;
+  const long cap = 2L * ncu;
+  const int per = ncu * std::max(2, a.min_bpc);
+  const int tmax = std::min(a.tpb_req, (nb + per - 1) / per);
+  auto makespan = [&](long g) { return ((g + cap - 1) / cap) * ((nb + g - 1) / g); };
+  int best_g = nb;
+  long best = makespan(nb);
+  for (int t = 2; t <= tmax; ++t) {
+    const int g = ((nb + t - 1) / t + 7) / 8 * 8;
+    if (g >= nb) continue;
+    const long m = makespan(g);
+    if (m < best || (m == best && g < best_g)) {
+      best = m;
+      best_g = g;
+    }
+  }
+  if (best_g >= nb) return nb;
+  a.tpb = (nb + best_g - 1) / best_g;
+  return best_g;
+}
+
+// gemm_bf16_pp launch: persistent where the 8-phase family is (persistent_kernel), else one block per tile
+template <int L, int E, typename OutT, int ACT>
+constexpr bool persistent_kernel();
+template <int L, int E, typename OutT, int ACT>
+static void launch_pp_act(const GemmArgs& a0, hipStream_t s) {
+  const int nb0 = (a0.M / BT_M) * (a0.N / PP_BN) * a0.ksplit;
+  if constexpr (persistent_kernel<L, E, OutT, ACT>()) {
+    GemmArgs a = a0;
+    const int nb = grid_pp(a, nb0, a0.K / BT_K / a0.ksplit);
+    if (a.tpb > 1) {
+      hipLaunchKernelGGL((gemm_bf16_pp<L, E, OutT, ACT, true>), dim3(nb), dim3(256), 0, s, a);
+      return;
+    }
+  }
+  GemmArgs a = a0;
+  a.tpb = 1;
+  hipLaunchKernelGGL((gemm_bf16_pp<L, E, OutT, ACT>), dim3(nb0), dim3(256), 0, s, a);
+}
+template <int L, int E, typename OutT>
+static void launch_pp(const GemmArgs& a, hipStream_t s) {
+  constexpr bool fwd = L == L_NT && (E == EPI_ACT || E == EPI_GLU);
+  constexpr bool bwd = L == L_NN && (E == EPI_DACT || E == EPI_DGLU);
+  if constexpr ((fwd || bwd) && std::is_same<OutT, uint16_t>::value) {
+    switch (a.act) {
+      case ACT_RELU: launch_pp_act<L, E, OutT, ACT_RELU>(a, s); return;
+      case ACT_SILU: launch_pp_act<L, E, OutT, ACT_SILU>(a, s); return;
+      case ACT_GELU: launch_pp_act<L, E, OutT, ACT_GELU>(a, s); return;
+      default: break;
+    }
+  }
+  launch_pp_act<L, E, OutT, -1>(a, s);
+}
+
 // main kernel writes partials into the workspace, then the reduction applies the epilogue
 template <int L, int E>
 static hipError_t launch_splitk(const GemmArgs& a, int out_dt, float* ws, hipStream_t s) {
@@ -1656,7 +1723,8 @@ static hipError_t launch_splitk(const GemmArgs& a, int out_dt, float* ws, hipStr
   w.beta = 0.f;
   const int nb = (a.M / BT_M) * (a.N / BT_N) * a.ksplit;
   w.tpb = 1;
-  if (a.variant == 4) hipLaunchKernelGGL((gemm_bf16_8ph<L, EPI_STORE, float, true, -1, 4>), dim3(nb), dim3(512), 0, s, w);
+  if (a.variant == 5) launch_pp<L, EPI_STORE, float>(w, s);
+  else if (a.variant == 4) hipLaunchKernelGGL((gemm_bf16_8ph<L, EPI_STORE, float, true, -1, 4>), dim3(nb), dim3(512), 0, s, w);
   else hipLaunchKernelGGL((gemm_bf16_8ph<L, EPI_STORE, float, true>), dim3(nb), dim3(512), 0, s, w);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
@@ -1721,6 +1789,11 @@ static hipError_t launch_bf16(const GemmArgs& a, int out_dt, hipStream_t s) {
   if (v == 0) v = (a.K % (2 * BT_K) == 0) ? 3 : 1;
   if (v >= 2 && a.K % (2 * BT_K) != 0) v = 1;
   const bool f32 = out_dt == DT_F32;
+  if (a.variant == 5) {  // 256x128 tiles, two blocks per CU (gemm_pp.h)
+    if (f32) launch_pp<L, E, float>(a, s);
+    else launch_pp<L, E, uint16_t>(a, s);
+    return hipGetLastError();
+  }
   if (v == 1) {
     if (f32) hipLaunchKernelGGL((gemm_bf16_256<L, E, float>), dim3(nb), dim3(512), 0, s, a);
     else hipLaunchKernelGGL((gemm_bf16_256<L, E, uint16_t>), dim3(nb), dim3(512), 0, s, a);
@@ -1784,7 +1857,9 @@ static hipError_t dispatch_opt(int path, const GemmArgs& a, int in_dt, hipStream
   if (path == 0 && a.ksplit > 1) return launch_splitk<L_TN, E>(a, DT_F32, a.ws, s);
   if (path == 0) {
     const int nb = (a.M / BT_M) * (a.N / BT_N);
-    if (a.K % (2 * BT_K) == 0 && a.variant == 4)
+    if (a.variant == 5)
+      launch_pp<L_TN, E, float>(a, s);
+    else if (a.K % (2 * BT_K) == 0 && a.variant == 4)
       hipLaunchKernelGGL((gemm_bf16_8ph<L_TN, E, float, true, -1, 4>), dim3(nb), dim3(512), 0, s, a);
     else if (a.K % (2 * BT_K) == 0 && a.variant != 1)
       launch_8ph_act<L_TN, E, float, -1, 8>(a, nb, s);

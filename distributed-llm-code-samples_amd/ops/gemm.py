@@ -183,13 +183,15 @@ def choose_ksplit(M: int, N: int, K: int) -> int:
     fp32 round trip through HBM)."""
     if not _SPLITK["enabled"] or M % 256 or N % 256 or K % 128:
         return 1
-    tiles = (M // 256) * (N // 256)
-    if tiles >= NUM_CUS * 0.75:
+    pp = _VARIANT["name"] == "pp"   # 256x128 tiles, two resident blocks per CU
+    tiles = (M // 256) * (N // (128 if pp else 256))
+    slots = NUM_CUS * (2 if pp else 1)
+    if tiles >= slots * 0.75:
         return 1
 
     def util(s):
         blocks = tiles * s
-        return blocks / (-(-blocks // NUM_CUS) * NUM_CUS)
+        return blocks / (-(-blocks // slots) * slots)
 
     best, best_u = 1, util(1)
     for s in (2, 3, 4, 6, 8):
@@ -316,7 +318,8 @@ def relu_mask_bytes(M: int, N: int) -> int:
 def relu_mask_supported(M: int, N: int, K: int, dtype: torch.dtype = torch.bfloat16) -> bool:
     """Whether the forward (``x·W1ᵀ``, K = D) / dgrad (``dy·W2``, K = D) pair of an ``[M, N]`` ReLU activation runs
     on the 8-phase kernels that share the bitmask's tile-native layout."""
-    return (dtype == torch.bfloat16 and M % 256 == 0 and N % 256 == 0 and K % 128 == 0
+    kstep = 64 if _VARIANT["name"] == "pp" else 128
+    return (dtype == torch.bfloat16 and M % 256 == 0 and N % 256 == 0 and K % kstep == 0
             and choose_ksplit(M, N, K) == 1 and _VARIANT["name"] != "2stage")
 
 
@@ -326,7 +329,8 @@ def _mask_ptr(mask: torch.Tensor, M: int, N: int) -> int:
     return mask.data_ptr()
 
 
-BF16_VARIANTS = {"auto": 0, "2stage": 1, "8phase": 2, "8phase_stagger": 3, "4phase_stagger": 4}
+# "pp": 256x128 tiles, 4 waves, 80 KiB LDS -> two blocks per CU (csrc/gemm_pp.h); the others are 256x256 main loops
+BF16_VARIANTS = {"auto": 0, "2stage": 1, "8phase": 2, "8phase_stagger": 3, "4phase_stagger": 4, "pp": 5}
 
 
 def set_bf16_variant(name: str) -> str:

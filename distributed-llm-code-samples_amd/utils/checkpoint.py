@@ -282,14 +282,16 @@ def _consolidated_sources(path: str, meta: dict, reader: _Reader) -> dict:
                     ((0, Fx, 0, Dx),
                      lambda a, b, c, d, k=key1, fn=fname: reader.slice(fn, k, (slice(a, b), slice(c, d)))))
             else:
-                cache = {}
-
-                def read13(a, b, c, d, l=l, pre=pre, fn=fname, cache=cache):
-                    if "g" not in cache:
-                        w1 = reader.slice(fn, f"{pre}.{l}.w1", slice(None))
-                        w3 = reader.slice(fn, f"{pre}.{l}.w3", slice(None))
-                        cache["g"] = interleave_w13(w1, w3)
-                    return cache["g"][a:b, c:d]
+                def read13(a, b, c, d, l=l, pre=pre, fn=fname):
+                    # interleaved rows [a, b) lie in 2*GLU_BLOCK-row periods p0 .. p1-1, i.e. logical rows
+                    # [p0*GLU_BLOCK, p1*GLU_BLOCK) of w1 and of w3: slice only those (and columns [c, d)), re-interleave,
+                    # crop.  Reads (b - a) rows + < 2 periods, never the whole tensors.
+                    per = 2 * GLU_BLOCK
+                    p0, p1 = a // per, -(-b // per)
+                    rows = slice(p0 * GLU_BLOCK, p1 * GLU_BLOCK)
+                    w1 = reader.slice(fn, f"{pre}.{l}.w1", (rows, slice(c, d)))
+                    w3 = reader.slice(fn, f"{pre}.{l}.w3", (rows, slice(c, d)))
+                    return interleave_w13(w1, w3)[a - p0 * per:b - p0 * per]
 
                 src.setdefault((bname, l, "w1"), []).append(((0, 2 * Fx, 0, Dx), read13))
     return src
@@ -309,6 +311,10 @@ def load_into(eng, path: str) -> tuple[dict, int]:
         src = _consolidated_sources(path, meta, reader)
     if meta["layers"] != eng.L or bool(meta["gated"]) != bool(eng.gated):
         raise ValueError(f"checkpoint is L={meta['layers']} gated={meta['gated']}, engine L={eng.L} gated={eng.gated}")
+    # a larger checkpoint would contain every needed box and silently load a sub-block of the wrong-sized matrices
+    for dim in ("D", "F"):
+        if meta.get(dim) is not None and int(meta[dim]) != int(getattr(eng, dim)):
+            raise ValueError(f"checkpoint has {dim}={meta[dim]}, engine {dim}={getattr(eng, dim)}")
     bufs = eng.flat_buffers()
     for bname, target in bufs.items():
         for e in eng.entries:

@@ -25,8 +25,10 @@ def _round_up(n: int, a: int) -> int:
 def plan(D: int, F: int, L: int, tokens: int, dp: int = 1, tp: int = 1, mode: str = "none", gated: bool = False,
          act: str = "relu", dtype: str = "bf16", grad_dtype: str = "bf16", optimizer: str = "sgd",
          recompute: str = "none", relu_mask: bool = True, sequence_parallel: bool = False,
-         align: int = 64) -> dict:
-    """Per-rank bytes by buffer (and GiB totals).  ``mode``: none | ddp | zero | fsdp (over ``dp`` ranks)."""
+         align: int = 64, wgrad_stream: bool = False) -> dict:
+    """Per-rank bytes by buffer (and GiB totals).  ``mode``: none | ddp | zero | fsdp (over ``dp`` ranks).
+    ``wgrad_stream``: the concurrent weight-gradient stream (single device, fused optimizer, kept activations, no
+    TP) rotates two dgrad and three dx buffers instead of one and two (``FFNTrainer.da_ring`` / ``dxb``)."""
     cd = 2 if dtype == "bf16" else 4
     gd = 2 if grad_dtype == "bf16" else 4
     multi = dp > 1
@@ -63,8 +65,9 @@ def plan(D: int, F: int, L: int, tokens: int, dp: int = 1, tp: int = 1, mode: st
         b["preactivations"] = nA * T * R1 * cd
     if relu_mask and act == "relu" and not gated and dtype == "bf16":
         b["relu_masks"] = nA * (T // 256) * (F_loc // 256) * 8192
-    b["dgrad_buffer"] = T * R1 * cd
-    b["dx_buffers"] = 2 * T * D * cd
+    ws = wgrad_stream and fused and tp == 1 and keep and not sp
+    b["dgrad_buffer"] = (2 if ws else 1) * T * R1 * cd
+    b["dx_buffers"] = (3 if ws else 2) * T * D * cd
     if sp:
         b["sp_buffers"] = (3 + (L if keep else 0)) * T * D * cd + 2 * Tl * D * cd
     state = sum(v for k, v in b.items() if k in ("master_fp32", "compute_copy", "grads", "adam_moments",

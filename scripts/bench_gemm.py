@@ -59,6 +59,8 @@ def main():
     dx = torch.empty(T, D, device=dev, dtype=bf)
     gw1 = torch.empty(F, D, device=dev, dtype=torch.float32)
     gw2 = torch.empty(D, F, device=dev, dtype=torch.float32)
+    mw2 = torch.randn(D, F, device=dev, dtype=torch.float32) * 0.02   # fp32 master + bf16 copy (fused SGD)
+    cw2 = mw2.to(bf)
     gm = a.group_m
     cases = {
         "fwd1 h=x.W1t (NT,act)": (lambda: gemm(x, w1, "nt", out=act, epi="act", act="relu", group_m=gm),
@@ -66,6 +68,8 @@ def main():
         "fwd2 y=a.W2t (NT)": (lambda: gemm(h, w2, "nt", out=y, group_m=gm), lambda: h @ w2.t()),
         "dW2=dyT.a (TN,f32)": (lambda: gemm(dy, h, "tn", out=gw2, group_m=gm),
                                lambda: (dy.t() @ h).float()),
+        "dW2 sgd (TN,fused)": (lambda: gemm(dy, h, "tn", out=mw2, epi="sgd", lr=1e-9, aux_out=cw2, group_m=gm),
+                               lambda: mw2.add_((dy.t() @ h).float(), alpha=-1e-9)),
         "da=dy.W2 (NN,dact)": (lambda: gemm(dy, w2, "nn", out=da, epi="dact", act="relu", aux=h, group_m=gm),
                                lambda: (dy @ w2) * (h > 0)),
         "dx=da.W1 (NN)": (lambda: gemm(h, w1, "nn", out=dx, group_m=gm), lambda: h @ w1),
@@ -84,6 +88,9 @@ def main():
                 if v.startswith("tpb"):
                     set_bf16_variant("8phase_stagger")
                     set_tiles_per_block(int(v[3:]))
+                elif v.startswith("pp"):   # 256x128 two-blocks-per-CU family; ppN: N tiles per persistent block
+                    set_bf16_variant("pp")
+                    set_tiles_per_block(int(v[2:] or 1))
                 else:
                     set_bf16_variant(v)
                     set_tiles_per_block(1)
@@ -102,7 +109,7 @@ def main():
         res[name] = row
         print(msg, flush=True)
     set_bf16_variant("auto")
-    set_tiles_per_block(2)
+    set_tiles_per_block(8)
     if a.json:
         with open(a.json, "w") as f:
             json.dump({"T": T, "D": D, "F": F, "cases": res}, f, indent=1)

@@ -104,3 +104,57 @@ def test_tp_chunk_policy_avoids_split_k_chunks():
     assert gpu_chunk_count(T, D, 14336 // 2, 14336, 4) == 2       # gated: R1 = 2 F_loc
     assert gpu_chunk_count(4 * T, D, 16384 // 2, 16384 // 2, 4) == 4
     assert gpu_chunk_count(T, D, 8192, 8192, 1) == 1
+
+
+def _engine(D=16, F=64, L=2, gated=False, act="relu"):
+    cfg = TrainConfig(model=ModelConfig(D, F, L, act, gated), batch_size=1, seq_len=32, lr=1e-2)
+    eng = FFNTrainer(cfg, Mesh(), torch.device("cpu"))
+    gen = torch.Generator().manual_seed(5)
+    eng.load_full_params([init_ffn_layer(D, F, gen, gated) for _ in range(L)])
+    return eng
+
+
+@pytest.mark.parametrize("fmt", ["consolidated", "sharded"])
+@pytest.mark.parametrize("dim", ["D", "F"])
+def test_checkpoint_rejects_other_model_dims(fmt, dim, tmp_path):
+    """A checkpoint of a LARGER model contains every box a smaller engine needs; resuming from it must raise, not
+    silently load a sub-block of the wrong-sized matrices."""
+    from dllm.utils.checkpoint import load_checkpoint, save_checkpoint
+
+    save_checkpoint(_engine(D=32, F=128) if dim == "D" else _engine(F=128), str(tmp_path), step=1, fmt=fmt)
+    with pytest.raises(ValueError, match=f"{dim}="):
+        load_checkpoint(_engine(D=16, F=64), str(tmp_path))
+    load_checkpoint(_engine(D=32, F=128) if dim == "D" else _engine(F=128), str(tmp_path))  # same dims: fine
+
+
+def test_gated_consolidated_reads_only_needed_rows(tmp_path):
+    """A gated consolidated checkpoint stores w1 / w3 separately; the loader rebuilds the interleaved storage rows
+    [a, b) from just the w1 / w3 rows (and columns) that cover them, not from the whole tensors."""
+    from dllm.models.ffn import interleave_w13
+    from dllm.utils.checkpoint import _consolidated_sources, _Reader, save_checkpoint
+
+    eng = _engine(D=16, F=128, L=1, gated=True, act="silu")
+    save_checkpoint(eng, str(tmp_path), step=0)
+    full = eng.gather_full_params()[0]
+    meta = {"layers": 1, "gated": True, "D": 16, "F": 128}
+    reader = _Reader(str(tmp_path))
+    (_, read), = _consolidated_sources(str(tmp_path), meta, reader)[("params", 0, "w1")]
+    got = read(40, 70, 4, 12)
+    torch.testing.assert_close(got, interleave_w13(full["w1"], full["w3"])[40:70, 4:12], rtol=0, atol=0)
+    # rows 40..69 lie in 32-row periods 1..2 -> w1 / w3 rows 16..47 (x 8 columns): 2 * 32 * 8 fp32 values
+    assert reader.bytes_read == 2 * 32 * 8 * 4, reader.bytes_read
+
+
+def test_sizing_counts_wgrad_stream_buffers():
+    """The concurrent weight-gradient stream rotates 2 dgrad and 3 dx buffers (engine da_ring / dxb); the planner
+    counts them only where the engine enables the stream (single device, fused optimizer, kept activations)."""
+    from dllm.utils.sizing import plan
+
+    kw = dict(dtype="bf16", grad_dtype="bf16")
+    base = plan(64, 256, 2, 128, **kw)["bytes"]
+    ws = plan(64, 256, 2, 128, wgrad_stream=True, **kw)["bytes"]
+    assert ws["dgrad_buffer"] == 2 * base["dgrad_buffer"] and ws["dx_buffers"] == 3 * 128 * 64 * 2
+    for off in (dict(dp=2, mode="ddp"), dict(tp=2), dict(recompute="full")):
+        a = plan(64, 256, 2, 128, wgrad_stream=True, **kw, **off)["bytes"]
+        b = plan(64, 256, 2, 128, **kw, **off)["bytes"]
+        assert a["dgrad_buffer"] == b["dgrad_buffer"] and a["dx_buffers"] == b["dx_buffers"]

@@ -39,7 +39,7 @@ def _ref(a, b, layout):
     return {"nt": lambda: a @ b.t(), "nn": lambda: a @ b, "tn": lambda: a.t() @ b}[layout]()
 
 
-@pytest.fixture(params=["2stage", "8phase", "8phase_stagger", "4phase_stagger"])
+@pytest.fixture(params=["2stage", "8phase", "8phase_stagger", "4phase_stagger", "pp"])
 def variant(request):
     old = set_bf16_variant(request.param)
     yield request.param
@@ -365,12 +365,20 @@ def test_splitk_matches_unsplit(layout, epi):
         torch.testing.assert_close(x.float(), y.float(), rtol=tol, atol=tol * float(y.float().abs().max() + 1e-30))
 
 
+@pytest.fixture(params=["8phase_stagger", "pp"])
+def family(request):
+    """The two persistent-capable bf16 families: 256x256 8-phase (one block per CU) and 256x128 (two per CU)."""
+    old = set_bf16_variant(request.param)
+    yield request.param
+    set_bf16_variant(old)
+
+
 @pytest.mark.parametrize("tpb", [2, 3, 64])
 @pytest.mark.parametrize("layout,epi", [("nt", "act"), ("nt", "store"), ("nn", "dact"), ("nn", "store"),
                                         ("tn", "sgd"), ("tn", "adam"), ("tn", "store_f32"), ("nt", "glu")])
-def test_persistent_blocks_bitwise_equal(tpb, layout, epi):
-    """Persistent 8-phase blocks (several tiles per block, next tile prefetched under the epilogue) give
-    bitwise the same results as one block per tile: same tiles, same K order, same epilogue."""
+def test_persistent_blocks_bitwise_equal(tpb, layout, epi, family):
+    """Persistent blocks (several tiles per block, next tile prefetched under the epilogue) give bitwise the same
+    results as one block per tile: same tiles, same K order, same epilogue."""
     from dllm.ops.gemm import set_tiles_per_block
 
     # 1000 tiles: persistent grids with uneven blocks for every cap (tpb 2: 504 blocks, 496 with two tiles and 8
@@ -410,7 +418,7 @@ def test_persistent_blocks_bitwise_equal(tpb, layout, epi):
 
 
 @pytest.mark.parametrize("layout", ["nt", "tn"])
-def test_persistent_blocks_splitk_bitwise_equal(layout):
+def test_persistent_blocks_splitk_bitwise_equal(layout, family):
     """Persistent blocks over split-K slices (slot = tile x slice) == one block per slice, bitwise."""
     from dllm.ops.gemm import choose_ksplit, set_tiles_per_block
 
@@ -430,7 +438,7 @@ def test_persistent_blocks_splitk_bitwise_equal(layout):
 
 
 @pytest.mark.parametrize("tpb", [1, 2])
-def test_relu_mask_matches_activation_path(tpb):
+def test_relu_mask_matches_activation_path(tpb, family):
     """ReLU bitmask written by the forward GEMM and read by the dgrad == dgrad masked by the stored
     activation, bitwise (incl. -0 for negative masked values); forward output unchanged."""
     from dllm.ops.gemm import relu_mask_bytes, relu_mask_supported, set_tiles_per_block
@@ -472,10 +480,10 @@ def test_relu_mask_rejected_off_the_8phase_path():
 
 @pytest.mark.parametrize("layout,M,N,K", [("nt", 4352, 8448, 384), ("nn", 2048, 4096, 1024), ("tn", 2560, 3072, 2048),
                                           ("tn", 512, 512, 2048)])
-def test_race_screen_repeated_runs_bitwise(layout, M, N, K):
+def test_race_screen_repeated_runs_bitwise(layout, M, N, K, family):
     """Kernel race screen (cdna_hip_programming.md §5 race screens): the LDS-DMA pipeline, the staggered
     barriers and the persistent slot loop must give bitwise-identical results on every run, with random data,
-    across persistent (> 2 tiles / CU), one-tile and split-K grids."""
+    across persistent (> 2 tiles / CU), one-tile and split-K grids, for both kernel families."""
     a, b = _operands(layout, M, N, K, torch.bfloat16, seed=M + K)
     a, b = a.cuda(), b.cuda()
     first = gemm(a, b, layout, out_dtype=torch.float32)
