@@ -116,10 +116,12 @@ def parse(argv=None):
     p.add_argument("--tp_allreduce", choices=["rccl", "custom"], default="rccl",
                    help="TP activation all-reduce: RCCL, or the custom two-shot xGMI peer all-reduce (csrc/car.hip)")
     p.add_argument("--gemm_variant", default="auto",
-                   choices=["auto", "2stage", "8phase", "8phase_stagger", "4phase_stagger"],
-                   help="bf16 GEMM main-loop schedule (auto = 8-phase staggered when K % 128 == 0)")
+                   choices=["auto", "2stage", "8phase", "8phase_stagger", "4phase_stagger", "pp"],
+                   help="bf16 GEMM main-loop schedule (auto = 8-phase staggered when K % 128 == 0; pp = 256x128 tiles, "
+                        "two blocks per CU)")
     p.add_argument("--tpb", type=int, default=0,
-                   help="tiles per persistent 8-phase GEMM block (0 = auto: 2, or 1 for gated stacks; 1 = off)")
+                   help="cap on tiles per persistent GEMM block (0 = auto: 8, the launcher picks the makespan-optimal "
+                        "count under it; 1 = one block per tile)")
     p.add_argument("--min_bpc", type=int, default=0,
                    help="minimum blocks per CU of persistent GEMM grids (0 = auto: 2 with overlapping collectives)")
     p.add_argument("--wgrad_stream", action=argparse.BooleanOptionalAction, default=True,
@@ -188,18 +190,32 @@ def run_method(a, method: str, n: int, world: int, dev: torch.device, steps: int
     """Build the engine for ``method`` on ``n`` ranks, run ``warmup`` untimed + ``steps`` timed steps (+ the
     observed steps), return the method's record.  Collective over all ranks."""
     cpu = dev.type == "cpu"
-    sync = (lambda: None) if cpu else torch.cuda.synchronize
     dp_mode, dp, tp = mesh_of(method, n, a.tp)
     cfg = TrainConfig(model=model, batch_size=a.batch_size, seq_len=a.seq_len, num_steps=steps, dtype=a.dtype,
                       grad_dtype=a.grad_dtype, optimizer=a.optimizer, dp_mode=dp_mode, dp=dp, tp=tp,
                       bucket_mb=a.bucket_mb, recompute=a.recompute, sequence_parallel=a.sequence_parallel,
                       data="device", force_comm=force_comm, comm_backend=a.comm,
+                      force_tp_comm=force_comm and method in ("tp", "hybrid"),
                       side_optimizer=a.side_opt if headline else 0, tp_allreduce=a.tp_allreduce,
                       relu_mask=not a.no_relu_mask, gemm_tiles_per_block=a.tpb, fp32_gemm=a.fp32_gemm,
                       gemm_min_bpc=a.min_bpc,
                       wgrad_stream=a.wgrad_stream and headline and not a.graph)
     mesh = Mesh.build(dp, tp, force=force_comm, comm_backend="torch" if cpu else a.comm,
                       device=None if cpu else dev)
+    try:
+        return _run_on_mesh(a, method, cfg, mesh, n, world, dev, steps, warmup, force_comm, model, observe_steps,
+                            headline)
+    except BaseException:
+        # error path (e.g. out of memory on one rank): abort this method's communicators, so they neither leak
+        # into the next method nor block in a synchronising teardown against peers that moved on
+        mesh.destroy(abort=True)
+        raise
+
+
+def _run_on_mesh(a, method, cfg, mesh, n, world, dev, steps, warmup, force_comm, model, observe_steps, headline):
+    cpu = dev.type == "cpu"
+    sync = (lambda: None) if cpu else torch.cuda.synchronize
+    dp, tp = cfg.dp, cfg.tp
     if not cpu:
         torch.cuda.reset_peak_memory_stats(dev)
     eng = FFNTrainer(cfg, mesh, dev)
@@ -360,8 +376,11 @@ def main(argv=None) -> int:
     def on_deadline() -> None:
         if not done["printed"]:
             side[current["m"] or "?"] = {"error": f"not finished within --side_deadline_s {a.side_deadline_s}"}
-            emit(record(f"side method {current['m']} cut off at the deadline"))
+            rec = record(f"side method {current['m']} cut off at the deadline")
+            rec["side_cut_off"] = current["m"] or "?"  # machine-readable: the headline is valid, a side method is not
+            emit(rec)
         sys.stdout.flush()
+        # the headline line is printed and valid: exit 0 so drivers keep it; side_cut_off marks the cut-off method
         os._exit(0)
 
     watchdog = None

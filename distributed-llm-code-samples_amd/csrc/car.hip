@@ -12,6 +12,13 @@
 //   4. barrier
 //   5. copy-out  : my OUT region -> my input tensor
 //
+// Zero-copy form (round 3, dllm_car_all_reduce_arena): the engine allocates the TP-exchanged activations (layer
+// outputs, input gradients) inside one "arena" laid out identically on every rank and mapped by every peer.  The
+// producing GEMM writes its partial straight into the arena, rank r sums chunk r of every peer's range IN PLACE and
+// writes the sum back into every peer's range, and the consumer reads the arena tensor itself: no copy-in, no
+// copy-out, no IN/OUT staging (release fences on every XCD -> barrier -> reduce-scatter + push -> barrier ->
+// acquire fences).
+//
 // i.e. a reduce-scatter and an all-gather in one pass each direction, both spread over all links.
 // Bulk-data visibility across devices relies on the kernel boundaries (HIP dispatches carry system-scope
 // acquire/release fences); the barrier kernels add explicit system-scope fences and atomics.  Every
@@ -41,6 +48,12 @@ struct State {
   bool opened[MAXR] = {};
   unsigned epoch = 0;
   int* err = nullptr;   // device error word (1 = barrier timeout)
+  // zero-copy arena (dllm_car_attach_arena): a caller-owned allocation laid out identically on every rank; the
+  // all-reduce runs in place on a byte range of it (no copy-in / copy-out)
+  char* arena = nullptr;
+  long arena_bytes = 0;
+  Ptrs peer_arena{};
+  char* arena_map[MAXR] = {};  // opened IPC bases (closed at destroy)
 };
 
 __device__ __forceinline__ void fence_release_sys() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, ""); }
@@ -145,6 +158,47 @@ __global__ __launch_bounds__(256) void rs_push_kernel(Ptrs peers, int n, long ou
   block_release();
 }
 
+// In-place variant over the zero-copy arena: rank r reads chunk r of every peer's range, sums in rank order and
+// writes the sum back into chunk r of every peer's range.  Only rank r touches chunk r (of any peer) in this
+// phase, so reading and overwriting the same addresses is race-free; the second barrier publishes the result.
+template <typename T>
+__global__ __launch_bounds__(256) void rs_inplace_kernel(Ptrs peers, int n, long off, long v0, long v1) {
+  block_acquire();
+  for (long v = v0 + blockIdx.x * (long)blockDim.x + threadIdx.x; v < v1; v += (long)gridDim.x * blockDim.x) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    uint4 in[MAXR];
+#pragma unroll
+    for (int p = 0; p < MAXR; ++p)
+      if (p < n) in[p] = ((const uint4*)(peers.p[p] + off))[v];
+#pragma unroll
+    for (int p = 0; p < MAXR; ++p)
+      if (p < n) V8<T>::add(acc, in[p]);
+    const uint4 r = V8<T>::pack(acc);
+#pragma unroll
+    for (int p = 0; p < MAXR; ++p)
+      if (p < n) ((uint4*)(peers.p[p] + off))[v] = r;
+  }
+  block_release();
+}
+
+// Device-wide cache maintenance around the in-place exchange, one fence per workgroup on a grid that covers every
+// XCD: `fence_kernel(.., release)` writes back the producing GEMM's dirty L2 lines before peers read the range
+// (every XCD's L2, not just the barrier kernel's); the acquire form, after the second barrier, drops stale lines of
+// the range that peers have just rewritten, and poisons the range with NaN if a barrier timed out (a stalled peer
+// never turns into a silently partial sum).
+__global__ __launch_bounds__(64) void fence_kernel(uint4* __restrict__ data, long n16, const int* err, int release) {
+  if (release) {
+    block_release();
+    return;
+  }
+  block_acquire();
+  if (err != nullptr && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+    const uint4 nan = uint4{0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n16; i += (long)gridDim.x * blockDim.x) data[i] = nan;
+    block_release();
+  }
+}
+
 }  // namespace car
 }  // namespace dllm
 
@@ -247,6 +301,83 @@ int dllm_car_all_reduce(void* st, void* data, long nbytes, int dtype, double tim
   return (int)hipGetLastError();
 }
 
+// ---- zero-copy arena ----------------------------------------------------------------------------------------
+// IPC handle of the allocation holding `ptr` (its base) + the byte offset of `ptr` inside it: works for a
+// caching-allocator sub-block as well as a whole allocation
+int dllm_car_arena_handle(void* ptr, char* out, int nbytes, long* offset) {
+  if (nbytes < (int)sizeof(hipIpcMemHandle_t)) return -1;
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  hipError_t e = hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)ptr);
+  if (e != hipSuccess) return (int)e;
+  hipIpcMemHandle_t h;
+  e = hipIpcGetMemHandle(&h, (void*)base);
+  if (e != hipSuccess) return (int)e;
+  memcpy(out, &h, sizeof(h));
+  *offset = (long)((char*)ptr - (char*)base);
+  return 0;
+}
+
+// attach this rank's arena and map every peer's (handles: n consecutive hipIpcMemHandle_t, offsets: n longs; own
+// entries ignored).  handles == nullptr: peers are set with dllm_car_set_peer_arena (single-process testing).
+int dllm_car_attach_arena(void* st, void* arena, long bytes, const char* handles, const long* offsets) {
+  State* s = (State*)st;
+  if (!arena || bytes <= 0 || ((uintptr_t)arena % 16)) return -1;
+  s->arena = (char*)arena;
+  s->arena_bytes = bytes;
+  s->peer_arena.p[s->rank] = s->arena;
+  if (handles == nullptr) return 0;
+  for (int p = 0; p < s->n; ++p) {
+    if (p == s->rank) continue;
+    hipIpcMemHandle_t h;
+    memcpy(&h, handles + p * sizeof(hipIpcMemHandle_t), sizeof(h));
+    void* base = nullptr;
+    const hipError_t e = hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) return (int)e;
+    s->arena_map[p] = (char*)base;
+    s->peer_arena.p[p] = (char*)base + offsets[p];
+  }
+  return 0;
+}
+
+int dllm_car_set_peer_arena(void* st, int peer, void* peer_arena) {
+  State* s = (State*)st;
+  if (peer < 0 || peer >= s->n) return -1;
+  s->peer_arena.p[peer] = (char*)peer_arena;
+  return 0;
+}
+
+// In-place sum all-reduce of arena bytes [off, off + nbytes) on every rank (same offsets everywhere): no copies.
+// release fences -> barrier -> in-place reduce-scatter + push -> barrier -> acquire fences (+ NaN poison on timeout)
+int dllm_car_all_reduce_arena(void* st, long off, long nbytes, int dtype, double timeout_s, void* stream) {
+  State* s = (State*)st;
+  if (!s->arena || off < 0 || nbytes <= 0 || nbytes % 16 || off % 16 || off + nbytes > s->arena_bytes ||
+      (dtype != 0 && dtype != 1))
+    return -1;
+  hipStream_t q = (hipStream_t)stream;
+  const long n16 = nbytes / 16;
+  const long ticks = (long)(timeout_s * 1e8);
+  const long sig_off = 2 * s->cap;
+  if (s->n == 1) return 0;  // a one-rank sum is the input
+  const int fgrid = 512;    // >= 2 workgroups per CU: every XCD's L2 gets its fence
+  hipLaunchKernelGGL(fence_kernel, dim3(fgrid), dim3(64), 0, q, (uint4*)nullptr, 0L, (const int*)nullptr, 1);
+  hipLaunchKernelGGL(barrier_kernel, dim3(1), dim3(64), 0, q, s->peers, s->rank, s->n, sig_off, ++s->epoch, ticks,
+                     s->err);
+  const long per = (n16 + s->n - 1) / s->n;
+  const long v0 = std::min(n16, per * s->rank), v1 = std::min(n16, v0 + per);
+  if (v1 > v0) {
+    const int g = (int)std::min<long>((v1 - v0 + 255) / 256, 1024);
+    if (dtype == 0)
+      hipLaunchKernelGGL(rs_inplace_kernel<uint16_t>, dim3(g), dim3(256), 0, q, s->peer_arena, s->n, off, v0, v1);
+    else
+      hipLaunchKernelGGL(rs_inplace_kernel<float>, dim3(g), dim3(256), 0, q, s->peer_arena, s->n, off, v0, v1);
+  }
+  hipLaunchKernelGGL(barrier_kernel, dim3(1), dim3(64), 0, q, s->peers, s->rank, s->n, sig_off, ++s->epoch, ticks,
+                     s->err);
+  hipLaunchKernelGGL(fence_kernel, dim3(fgrid), dim3(64), 0, q, (uint4*)(s->arena + off), n16, (const int*)s->err, 0);
+  return (int)hipGetLastError();
+}
+
 // 0 = ok, 1 = a barrier timed out (read after synchronising the stream); sticky until destroy
 int dllm_car_error(void* st) {
   State* s = (State*)st;
@@ -259,8 +390,10 @@ int dllm_car_destroy(void* st) {
   State* s = (State*)st;
   if (!s) return 0;
   (void)hipDeviceSynchronize();
-  for (int p = 0; p < s->n; ++p)
+  for (int p = 0; p < s->n; ++p) {
     if (s->opened[p]) (void)hipIpcCloseMemHandle(s->peers.p[p]);
+    if (s->arena_map[p]) (void)hipIpcCloseMemHandle(s->arena_map[p]);
+  }
   (void)hipFree(s->buf);
   (void)hipFree(s->err);
   delete s;

@@ -1748,8 +1748,9 @@ static hipError_t launch_splitk(const GemmArgs& a, int out_dt, float* ws, hipStr
 template <int L, int E, typename OutT, int ACT>
 constexpr bool persistent_kernel() {
   constexpr bool bf = std::is_same<OutT, uint16_t>::value;
-  if constexpr (L == L_NT) return bf && ((E == EPI_ACT && ACT == ACT_RELU) || E == EPI_STORE);
-  if constexpr (L == L_NN) return bf && ((E == EPI_DACT && ACT == ACT_RELU) || E == EPI_STORE);
+  // gated (SwiGLU) stacks: the GLU forward / DGLU dgrad with a compile-time activation (round 3)
+  if constexpr (L == L_NT) return bf && ((E == EPI_ACT && ACT == ACT_RELU) || E == EPI_STORE || (E == EPI_GLU && ACT >= 0));
+  if constexpr (L == L_NN) return bf && ((E == EPI_DACT && ACT == ACT_RELU) || E == EPI_STORE || (E == EPI_DGLU && ACT >= 0));
   return E == EPI_STORE || E == EPI_SGD;
 }
 

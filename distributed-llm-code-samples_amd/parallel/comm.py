@@ -64,9 +64,33 @@ def _active(group) -> bool:
     return group is not None and dist.is_initialized()
 
 
+_COUNTS: dict | None = None
+
+
+class count_collectives:
+    """Context manager counting the collectives issued through this module, per group object (any backend,
+    CPU or GPU): ``with count_collectives() as c: ...; c.by_role(mesh.groups)``."""
+
+    def __enter__(self):
+        global _COUNTS
+        self.counts = _COUNTS = {}
+        return self
+
+    def __exit__(self, *exc):
+        global _COUNTS
+        _COUNTS = None
+        return False
+
+    def by_role(self, groups: dict) -> dict:
+        """{role: count} for a mesh's role groups (roles sharing one group object share its count)."""
+        return {r: self.counts.get(id(g), 0) for r, g in groups.items() if g is not None}
+
+
 def _issue(group, fn):
     """Run ``fn()`` (which issues one collective and returns its work); with a ``CommObserver`` active the
     collective's issue and completion are recorded (utils/observe.py)."""
+    if _COUNTS is not None:
+        _COUNTS[id(group)] = _COUNTS.get(id(group), 0) + 1
     obs = observe.active()
     if obs is None:
         return fn()

@@ -55,6 +55,12 @@ def _round_up(n: int, a: int) -> int:
     return (n + a - 1) // a * a
 
 
+def _nullctx():
+    from contextlib import nullcontext
+
+    return nullcontext()
+
+
 @dataclass
 class Entry:
     layer: int
@@ -78,7 +84,7 @@ class _Hooks:
 
     def after_dx(self, dx):
         e = self.eng
-        if e.mesh.tp > 1:
+        if e.tp_comm:
             if e.tp_car is not None:
                 self.tp_work = e.tp_car.all_reduce_async(dx)
             else:
@@ -129,7 +135,10 @@ class FFNTrainer:
         if self.fsdp and (self.R1 % d or D % d):
             raise ValueError(f"FSDP needs W1 rows ({self.R1}) and D ({D}) divisible by dp={d} (train_ffns.py:266)")
         self.cd, self.gd = cfg.torch_dtype, cfg.torch_grad_dtype
-        self.sp = cfg.sequence_parallel and t > 1
+        # TP collectives: a real tp axis, or forced over the size-1 tp communicator (force_tp_comm, single-GPU
+        # check of the TP path: the same collectives, streams and waits as tp > 1)
+        self.tp_comm = t > 1 or (cfg.force_comm and cfg.force_tp_comm and mesh.group("tp") is not None)
+        self.sp = cfg.sequence_parallel and self.tp_comm
         T = cfg.tokens
         if self.sp and T % t:
             raise ValueError("sequence parallelism needs tokens % tp == 0")
@@ -150,8 +159,12 @@ class FFNTrainer:
         if cfg.tp_allreduce == "custom" and t > 1 and self.device.type == "cuda" and not cfg.sequence_parallel:
             from .car import CustomAllReduce
 
-            self.tp_car = CustomAllReduce(mesh.tp_ranks, self.device, cap_bytes=cfg.tokens * D * 4,
-                                          tag=f"tp{mesh.dp_rank}")
+            # zero-copy: the exchanged activations (layer outputs xs[1..L], input gradients dxb) live in the car's
+            # arena, which every TP peer maps; GEMMs write partials there and the all-reduce runs in place
+            es = torch.empty(0, dtype=cfg.torch_dtype).element_size()
+            per = (cfg.tokens * D * es + 255) // 256 * 256
+            self.tp_car = CustomAllReduce(mesh.tp_ranks, self.device, cap_bytes=4096, tag=f"tp{mesh.dp_rank}",
+                                          arena_bytes=(L + 3) * per)
             mesh.groups["tp_car"] = self.tp_car
 
         # ---- flat owned parameter layout (completion order) ------------------------------------
@@ -224,14 +237,19 @@ class FFNTrainer:
                           for _ in range(2)]
             self.gring = [{n: torch.empty(full[n], dtype=self.gd, device=dev) for n in ("w2", "w1")}
                           for _ in range(2)]
-            self.ag_work = [None, None]
+            self.ag_work = [None, None]     # per slot: {name: work} of the in-flight gather (None: landed)
             self.ag_layer = [-1, -1]
-            self.rs_pending = [None, None]  # (layer, [works])
+            self.rs_pending = [None, None]  # per slot: (layer, {name: work}) -- one reduce-scatter per weight
+            self.ag_next = set()            # layers whose post-update gather for the next forward is in flight
+            self.fsdp_stream = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
+            self.fsdp_tail_ev = None
 
         # ---- activations -------------------------------------------------------------------------
         Tl = T // t if self.sp else T  # tokens held per rank between layers
         self.Tl = Tl
-        self.xs = [None] + [torch.empty((Tl, D), dtype=self.cd, device=dev) for _ in range(L)]
+        car_arena = self.tp_car is not None and self.tp_car.arena is not None
+        self.xs = [None] + [self.tp_car.arena_view((Tl, D), self.cd) if car_arena else
+                            torch.empty((Tl, D), dtype=self.cd, device=dev) for _ in range(L)]
         keep = cfg.recompute == "none"
         nA = L if keep else 1
         self.acts_a = [torch.empty((T, self.F_loc), dtype=self.cd, device=dev) for _ in range(nA)]
@@ -256,7 +274,7 @@ class FFNTrainer:
         c = max(1, cfg.tp_chunks)
         if dev.type == "cuda":
             c = gpu_chunk_count(T, D, self.F_loc, self.R1, c)
-        if t > 1 and not self.sp and c > 1 and T % (256 * c) == 0 and L > 1:
+        if self.tp_comm and not self.sp and c > 1 and T % (256 * c) == 0 and L > 1:
             if self.masks is None:
                 self.tp_chunks = c
             else:
@@ -284,13 +302,14 @@ class FFNTrainer:
         # last reads the weight they update; da / dx buffers rotate so the side stream's reads never race
         # the next layers' writes
         self.wg_stream = None
-        if (cfg.wgrad_stream and self.fused_opt and dev.type == "cuda" and t == 1 and not self.sp
+        if (cfg.wgrad_stream and self.fused_opt and dev.type == "cuda" and not self.tp_comm and not self.sp
                 and cfg.recompute == "none"):
             self.wg_stream = torch.cuda.Stream(device=dev)
             self.da_ring = [self.da, torch.empty_like(self.da)]
             self.da_free = [None, None]
             self.dx_free = [None, None, None]
-        self.dxb = [torch.empty((T, D), dtype=self.cd, device=dev)
+        self.dxb = [self.tp_car.arena_view((T, D), self.cd) if car_arena else
+                    torch.empty((T, D), dtype=self.cd, device=dev)
                     for _ in range(3 if self.wg_stream is not None else 2)]
         if self.sp:
             self.xfull = torch.empty((T, D), dtype=self.cd, device=dev)       # gathered layer input
@@ -422,6 +441,7 @@ class FFNTrainer:
             self.zero_sync_state()
         self.side_sync()
         self.ddp_sync()
+        self.fsdp_sync()
         out = {"params": self.master}
         if self.cfg.optimizer == "adam":
             out["adam_m"], out["adam_v"] = self.adam_m, self.adam_v
@@ -453,11 +473,17 @@ class FFNTrainer:
                 self._view(target, e).copy_(src.to(torch.float32))
         if target is self.master and not self.shared_copy and not self.zero:
             cast_(self.master, self.copy)
+        if self.fsdp and target is self.master:
+            self.fsdp_sync()
+            self.ag_next.clear()  # gathered rings hold the old weights
 
     @torch.no_grad()
     def refresh_copy(self) -> None:
         """Recompute the compute-dtype working copy from the fp32 master after the master was written
         directly (checkpoint load).  ZeRO: every rank casts its shard and all-gathers (collective)."""
+        if self.fsdp:
+            self.fsdp_sync()
+            self.ag_next.clear()  # gathered rings hold the old weights
         if self.shared_copy:
             return
         if not self.zero:
@@ -485,6 +511,7 @@ class FFNTrainer:
         Collective over the dp group under FSDP."""
         self.side_sync()
         self.ddp_sync()
+        self.fsdp_sync()
         src = self.master if flat is None else flat
         if self.zero:
             self.zero_sync_state()
@@ -576,13 +603,15 @@ class FFNTrainer:
                 s, e, _ = self.buckets[b]
                 self.bucket_work[b] = comm.all_reduce(self.grads[s:e], self.mesh.group("dp_ar"), async_op=True)
                 self._next_bucket += 1
-        elif self.fsdp and name == self.layer_order(l)[1]:
+        elif self.fsdp:
+            # one reduce-scatter per weight, issued the moment its gradient GEMM is done: the first weight's
+            # collective runs under the layer's remaining GEMMs instead of waiting for both
             slot = l % 2
-            g = self.gring[slot]
-            # the layer's two gradient reduce-scatters as one group (native: one fused RCCL launch)
-            works = [comm.reduce_scatter_into_many([(self.grad_view(l, n), g[n]) for n in ("w2", "w1")],
-                                                   self.mesh.group("dp_rs"), async_op=True)]
-            self.rs_pending[slot] = (l, works)
+            w = comm.reduce_scatter_into(self.grad_view(l, name), self.gring[slot][name], self.mesh.group("dp_rs"),
+                                         async_op=True)
+            if self.rs_pending[slot] is None or self.rs_pending[slot][0] != l:
+                self.rs_pending[slot] = (l, {})
+            self.rs_pending[slot][1][name] = w
 
     def _zero_finish(self, b: int, side: bool = False) -> None:
         """Bucket b's reduce-scatter is done -> update the owned shard -> all-gather the new bf16 copy.
@@ -643,34 +672,72 @@ class FFNTrainer:
             self.ag_pending[b].wait()
             self.ag_pending[b] = None
 
-    def _fsdp_finish_rs(self, slot: int) -> None:
+    def _fsdp_finish_rs(self, slot: int, names=None) -> None:
+        """Wait for the slot's pending reduce-scatters (``names``: only those weights) and update their shards."""
         pend = self.rs_pending[slot]
         if pend is None:
             return
         l, works = pend
-        for w in works:
-            w.wait()
-        s, e = self._layer_range(l)
-        self._opt(s, e)
-        self.rs_pending[slot] = None
+        for n in [n for n in self.layer_order(l) if n in works and (names is None or n in names)]:
+            works.pop(n).wait()
+            e = self.entry[(l, n)]
+            self._opt(e.offset, e.offset + e.numel)
+        if not works:
+            self.rs_pending[slot] = None
 
-    def _fsdp_gather(self, l: int) -> None:
+    def _fsdp_gather(self, l: int, names=("w2", "w1")) -> None:
         slot = l % 2
         grp = self.mesh.group("dp_ag")
-        # the layer's W2 and W1 shard all-gathers as one group (native: one fused RCCL launch)
-        self.ag_work[slot] = [comm.all_gather_into_many([(self.wring[slot][n], self.copy_view(l, n))
-                                                         for n in ("w2", "w1")], grp, async_op=True)]
+        if self.ag_layer[slot] != l or self.ag_work[slot] is None:
+            self.ag_work[slot] = {}
+        # the weights' shard all-gathers as one group (native: one fused RCCL launch)
+        w = comm.all_gather_into_many([(self.wring[slot][n], self.copy_view(l, n)) for n in names], grp,
+                                      async_op=True)
+        for n in names:
+            self.ag_work[slot][n] = w
         self.ag_layer[slot] = l
 
-    def _fsdp_weights(self, l: int) -> tuple[torch.Tensor, torch.Tensor]:
+    def _fsdp_weight(self, l: int, name: str) -> torch.Tensor:
+        """Layer l's gathered weight ``name`` from the ring, after a (stream) wait for its gather."""
         slot = l % 2
         if self.ag_layer[slot] != l:
             raise RuntimeError(f"FSDP ring slot {slot} holds layer {self.ag_layer[slot]}, wanted {l}")
-        if self.ag_work[slot] is not None:
-            for w in self.ag_work[slot]:
-                w.wait()
-            self.ag_work[slot] = None
-        return self.wring[slot]["w1"], self.wring[slot]["w2"]
+        works = self.ag_work[slot]
+        if works is not None and works.get(name) is not None:
+            works.pop(name).wait()
+        return self.wring[slot][name]
+
+    def _fsdp_weights(self, l: int) -> tuple[torch.Tensor, torch.Tensor]:
+        return self._fsdp_weight(l, "w1"), self._fsdp_weight(l, "w2")
+
+    def _fsdp_tail(self) -> None:
+        """Step boundary of FSDP: the last two layers' gradients (layers 1 and 0) are reduce-scattered, their
+        shards updated and re-gathered for the next forward on a side stream, in the order the next forward needs
+        them: layer 0's first-completed weight (W1 without a layer-0 input gradient: its chain runs under the
+        dW2 GEMM), layer 1, then layer 0's other weight.  The forward then waits per weight (W1 before the first
+        GEMM, W2 before the second), so only the last chain's tail is exposed (reference: synchronous
+        reduce-scatter, gather at the start of the next forward, train_ffns.py:236-259, TODO :14/:252)."""
+        L = self.L
+        st = self.fsdp_stream
+        first, second = self.layer_order(0)
+        plan = [(0, (first,))] + ([(1, ("w2", "w1"))] if L >= 2 else []) + [(0, (second,))]
+        ctx = torch.cuda.stream(st) if st is not None else _nullctx()
+        with ctx:
+            for l, names in plan:
+                # the chain waits only for its reduce-scatters (ordered after the gradient GEMMs that wrote the
+                # grad ring, and after every earlier GEMM reading this layer's ring slot), not for the compute
+                # stream's later GEMMs
+                self._fsdp_finish_rs(l % 2, names)
+                self._fsdp_gather(l, names)
+                self.ag_next.add(l)
+            if st is not None:
+                self.fsdp_tail_ev = torch.cuda.Event()
+                self.fsdp_tail_ev.record(st)
+
+    def fsdp_sync(self) -> None:
+        """Make the current stream wait for the step-boundary updates / gathers (checkpoint, readout)."""
+        if self.fsdp and self.fsdp_stream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.fsdp_stream)
 
     # ------------------------------------------------------------------------------------------------
     # one training step
@@ -694,13 +761,19 @@ class FFNTrainer:
 
         # ---------------- forward ----------------
         mark = self._mark("forward")
-        if self.fsdp:
+        fsdp_w2 = None
+        if self.fsdp and 0 not in self.ag_next:
             self._fsdp_gather(0)
         for l in range(L):
             if self.fsdp:
-                w1, w2 = self._fsdp_weights(l)
-                if l + 1 < L:
+                w1 = self._fsdp_weight(l, "w1")   # W2 is waited for right before the second GEMM
+                w2 = self.wring[l % 2]["w2"]
+                self.ag_next.discard(l)
+                if l + 1 < L and (l + 1) not in self.ag_next:
                     self._fsdp_gather(l + 1)
+
+                def fsdp_w2(l=l):
+                    self._fsdp_weight(l, "w2")
             else:
                 if self.zero:
                     for b in self.weight_buckets[(l, "w1")]:
@@ -720,9 +793,11 @@ class FFNTrainer:
                     self._side_wait(l, "w2")
                 if self.ddp:
                     self._ddp_wait(l, "w2")
+                if fsdp_w2 is not None:
+                    fsdp_w2()
                 self._sp_fwd(l, self.xs_full[l] if keep else self.xfull, w1, w2, a, h)
             else:
-                before2 = None
+                before2 = fsdp_w2
                 if self.zero:
                     def before2(l=l):
                         for b in self.weight_buckets[(l, "w2")]:
@@ -738,7 +813,7 @@ class FFNTrainer:
                     continue
                 layer_fwd(self.xs[l], w1, w2, act, gated, a, h, self.xs[l + 1], before_fwd2=before2,
                           mask=self._mask(l))
-                if self.mesh.tp > 1:
+                if self.tp_comm:
                     if self.tp_car is not None:
                         w = self.tp_car.all_reduce_async(self.xs[l + 1])
                     else:
@@ -757,6 +832,10 @@ class FFNTrainer:
         # ---------------- backward ----------------
         mark = self._mark("backward")
         self._next_bucket = 0
+        if self.fsdp and self.fsdp_tail_ev is not None:
+            # the previous step's tail reduce-scatters read the gradient ring this backward rewrites
+            torch.cuda.current_stream(self.device).wait_event(self.fsdp_tail_ev)
+            self.fsdp_tail_ev = None
         if self.fsdp and L >= 2 and self.ag_layer[(L - 2) % 2] != L - 2:
             # the forward left layers L-1 and L-2 in the ring; weights do not change until the
             # optimizer runs, so the reference's re-gather of L-2 (:245) is skipped when still resident
@@ -811,7 +890,7 @@ class FFNTrainer:
                     recompute_fwd1(self.xs[l], w1, act, gated, a, h, mask=self._mask(l))
                 dx = layer_bwd(g, self.xs[l], w1, w2, act, gated, a, h, gw1, gw2, self.da,
                                self.dxb[l % 2] if need_dx else None, hooks, mask=self._mask(l),
-                               dx_first=self.mesh.tp > 1 and cfg.tp_overlap)
+                               dx_first=self.tp_comm and cfg.tp_overlap)
                 if dx is not None:
                     g = dx
             if self.zero:
@@ -848,8 +927,7 @@ class FFNTrainer:
                     self.bucket_work[b].wait()
                     self._opt(s, e)
         elif self.fsdp:
-            for slot in ((L - 1) % 2, L % 2):
-                self._fsdp_finish_rs(slot)
+            self._fsdp_tail()
         elif not self.fused_opt and not self.side_opt:
             self._opt(0, self.total)
         self._unmark(mark)

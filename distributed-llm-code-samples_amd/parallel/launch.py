@@ -75,8 +75,8 @@ def run_rank(rank: int, world: int, cfg_dict: dict, method: int, backend: str, p
         device = torch.device("cuda", torch.cuda.current_device())
     dp_mode, dp, tp = METHOD_MESH[method](world, opts)
     cfg.dp_mode, cfg.dp, cfg.tp = dp_mode, dp, tp
-    mesh = Mesh.build(dp, tp, separate_streams=cfg.separate_streams, comm_backend=cfg.comm_backend,
-                      device=device if device.type == "cuda" else None)
+    mesh = Mesh.build(dp, tp, separate_streams=cfg.separate_streams, force=cfg.force_comm,
+                      comm_backend=cfg.comm_backend, device=device if device.type == "cuda" else None)
     eng = FFNTrainer(cfg, mesh, device)
 
     seed = int(opts.get("seed", 0))
@@ -101,8 +101,13 @@ def run_rank(rank: int, world: int, cfg_dict: dict, method: int, backend: str, p
     limit = min(len(seed_list), stop_after)
     for k in range(start_step, min(start_step + depth, limit)):
         data.prefetch(int(seed_list[k]))
+    from contextlib import nullcontext
+
+    from .comm import count_collectives
+
+    counter = count_collectives() if opts.get("count_collectives") else nullcontext()
     try:
-        with maybe_profile(opts.get("profile", ""), rank):
+        with maybe_profile(opts.get("profile", ""), rank), counter:
             for i, s in enumerate(seed_list):
                 if i < start_step:
                     continue
@@ -151,6 +156,8 @@ def run_rank(rank: int, world: int, cfg_dict: dict, method: int, backend: str, p
                             "adam": eng.adam_m.numel() if getattr(eng, "adam_m", None) is not None else 0},
             "ckpt_bytes_read_max": read_max,
         }
+        if opts.get("count_collectives") and steps > 0:
+            rec["collectives_per_step"] = {r: c / steps for r, c in counter.by_role(mesh.groups).items()}
     if world > 1 or opts.get("force_dist"):
         import torch.distributed as dist
 

@@ -73,12 +73,15 @@ class TrainConfig:
                                      # stream, concurrent with the dgrad chain (CUs shared; epilogues overlap)
     gemm_min_bpc: int = 0            # persistent GEMM grids: minimum blocks per CU (0 = auto: 2 when collectives
                                      # overlap the GEMMs, else 1)
-    gemm_tiles_per_block: int = 0    # persistent 8-phase GEMM blocks (process-wide): tiles per block; 0 = auto
-                                     # (2 for plain FFN stacks, 1 for gated stacks, where it measured slower)
+    gemm_tiles_per_block: int = 0    # persistent GEMM blocks (process-wide): cap on tiles per block; 0 = auto
+                                     # (8 -- the launcher picks the makespan-optimal count under it)
     fused_optimizer: bool = True     # fuse SGD/Adam into the wgrad GEMM epilogue when no grad collective
     side_optimizer: int = 0          # >0 (no grad collective, SGD): wgrad GEMMs store grads and a side stream
                                      # applies SGD on this many workgroups, overlapped with the next GEMMs
     force_comm: bool = False         # run the DDP/FSDP collective path even at dp=1 (single-GPU RCCL check)
+    force_tp_comm: bool = False      # with force_comm: also run the TP/SP collectives (forward output all-reduce
+                                     # in chunks, deferred last-layer all-reduce, dx all-reduce / SP reduce-scatter
+                                     # and all-gathers) over the size-1 tp communicator (single-GPU RCCL check)
     comm_backend: str = "torch"      # torch (ProcessGroupNCCL/gloo) | native (csrc/comm.cpp RCCL layer)
     tp_allreduce: str = "rccl"       # TP activation all-reduce: rccl (role communicator) | custom (csrc/car.hip)
     debug_sync: bool = False         # race screen: wait every collective at issue + device sync per layer

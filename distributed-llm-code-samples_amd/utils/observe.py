@@ -116,7 +116,8 @@ class CommObserver:
         self._open = None
 
     # -- report ----------------------------------------------------------------------------------------
-    def summary(self, steps: int) -> dict:
+    def intervals(self) -> tuple[dict, list]:
+        """Raw (ms since observation start) collective intervals per role and GEMM intervals (diagnostics)."""
         torch.cuda.synchronize(self.device)
         t = lambda ev: self.t0.elapsed_time(ev)  # noqa: E731  (ms since observation start)
         per_role: dict[str, list[tuple[float, float]]] = {}
@@ -126,7 +127,11 @@ class CommObserver:
             s = max(s, last_end.get(role, s))  # queued behind the role's previous collective
             last_end[role] = max(e, last_end.get(role, e))
             per_role.setdefault(role, []).append((s, e))
-        gem = _union([(t(a), t(b)) for a, b in self.gemms])
+        return per_role, [(t(a), t(b)) for a, b in self.gemms]
+
+    def summary(self, steps: int) -> dict:
+        per_role, gemms = self.intervals()
+        gem = _union(gemms)
         allc = _union([iv for ivs in per_role.values() for iv in ivs])
         union_ms, hidden = _length(allc), _intersect(allc, gem)
         steps = max(1, steps)

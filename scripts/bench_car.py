@@ -2,8 +2,9 @@
 
 Not an xGMI measurement: the peers' buffers sit in the same HBM and the ranks' kernels share the CUs, so this
 prices the protocol (flag barriers, the two-shot reduce-scatter / all-gather passes, the copy-in and copy-out)
-and the small-message latency, not the links.  Prints one JSON line per (n, size): median us per call (max over
-ranks) and the algorithmic bandwidth 2(n-1)/n * bytes / time.
+and the small-message latency, not the links.  Prints one JSON line per (n, size, mode): median us per call (max over
+ranks) and the algorithmic bandwidth 2(n-1)/n * bytes / time.  Modes: "staged" (copy-in / exchange / copy-out around
+an ordinary tensor) and "arena" (zero-copy: the tensor lives in the peer-mapped arena and is all-reduced in place).
 
     python scripts/bench_car.py [--ranks 2,4] [--sizes_kib 64,1024,8192,65536]
 """
@@ -35,10 +36,15 @@ def _proc(rank, n, port, sizes, iters, q):
     dist.init_process_group("gloo", rank=rank, world_size=n)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    car = CustomAllReduce(list(range(n)), dev, cap_bytes=max(sizes), tag="bench")
+    car = CustomAllReduce(list(range(n)), dev, cap_bytes=max(sizes), tag="bench", arena_bytes=max(sizes))
     out = []
-    for nbytes in sizes:
-        t = torch.randn(nbytes // 2, device=dev).bfloat16()
+    for nbytes, mode in [(b, m) for b in sizes for m in ("staged", "arena")]:
+        if mode == "arena":  # zero-copy: the tensor lives in the mapped arena, all-reduced in place
+            car._arena_next = 0
+            t = car.arena_view((nbytes // 2,), torch.bfloat16)
+            t.copy_(torch.randn(nbytes // 2, device=dev))
+        else:                # staged: copy-in -> exchange -> copy-out around an ordinary tensor
+            t = torch.randn(nbytes // 2, device=dev).bfloat16()
         for _ in range(3):
             car.all_reduce(t)
         torch.cuda.synchronize()
@@ -53,7 +59,7 @@ def _proc(rank, n, port, sizes, iters, q):
             times.append(e0.elapsed_time(e1) * 1e3)
         us = torch.tensor([statistics.median(times)], dtype=torch.float64)
         dist.all_reduce(us, op=dist.ReduceOp.MAX)
-        out.append((nbytes, float(us.item())))
+        out.append((nbytes, mode, float(us.item())))
     car.check()
     car.destroy()
     dist.barrier()
@@ -78,8 +84,8 @@ def main():
         res = dict(q.get(timeout=300) for _ in range(n))
         for p in ps:
             p.join(timeout=60)
-        for nbytes, us in res[0]:
-            print(json.dumps({"ranks": n, "bytes": nbytes, "us_per_call": round(us, 1),
+        for nbytes, mode, us in res[0]:
+            print(json.dumps({"ranks": n, "bytes": nbytes, "mode": mode, "us_per_call": round(us, 1),
                               "algbw_GBps": round(2 * (n - 1) / n * nbytes / us / 1e3, 1),
                               "note": "ranks share one GPU (HBM, CUs): protocol cost, not xGMI"}), flush=True)
 

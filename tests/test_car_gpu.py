@@ -26,7 +26,7 @@ def _expected(xs):
 # queue and serialise behind a barrier -- measured as bounded-spin timeouts.)
 
 
-def _proc(rank, n, port, numel, dtype, q):
+def _proc(rank, n, port, numel, dtype, q, arena=False):
     import torch.distributed as dist
 
     from dllm.parallel.car import CustomAllReduce
@@ -35,12 +35,19 @@ def _proc(rank, n, port, numel, dtype, q):
     dist.init_process_group("gloo", rank=rank, world_size=n)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    car = CustomAllReduce(list(range(n)), dev, cap_bytes=numel * 4, tag="test")
+    car = CustomAllReduce(list(range(n)), dev, cap_bytes=numel * 4, tag="test",
+                          arena_bytes=2 * numel * 4 if arena else 0)
+    # arena: two tensors carved from the zero-copy arena (the second at a non-zero offset), all-reduced in place
+    views = [car.arena_view((numel,), dtype) for _ in range(2)] if arena else None
     ok = True
     for it in range(3):
         xs = [torch.randn(numel, generator=torch.Generator().manual_seed(1000 * it + r)).to(dtype) for r in range(n)]
         want = _expected(xs)
-        t = xs[rank].to(dev)
+        if arena:
+            t = views[it % 2]
+            t.copy_(xs[rank].to(dev))
+        else:
+            t = xs[rank].to(dev)
         dist.barrier()
         car.all_reduce(t)
         car.check()
@@ -51,12 +58,14 @@ def _proc(rank, n, port, numel, dtype, q):
     q.put((rank, ok))
 
 
+@pytest.mark.parametrize("arena", [False, True])
 @pytest.mark.parametrize("n,dtype", [(2, torch.bfloat16), (4, torch.float32), (3, torch.bfloat16)])
-def test_processes_ipc(n, dtype, free_port):
+def test_processes_ipc(n, dtype, arena, free_port):
+    """Staged (copy-in / copy-out) and zero-copy arena (in place on the peer-mapped range) all-reduces."""
     numel = (1 << 18) + 8
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_proc, args=(r, n, free_port, numel, dtype, q)) for r in range(n)]
+    ps = [ctx.Process(target=_proc, args=(r, n, free_port, numel, dtype, q, arena)) for r in range(n)]
     for p in ps:
         p.start()
     for p in ps:
@@ -87,7 +96,8 @@ def _tp_proc(rank, n, port, q):
                       lr=1e-2, dp=1, tp=n, tp_allreduce="custom", skip_input_grad=False)
     mesh = Mesh.build(1, n, device=dev)
     eng = FFNTrainer(cfg, mesh, dev)
-    assert eng.tp_car is not None
+    assert eng.tp_car is not None and eng.tp_car.arena is not None
+    assert eng.tp_car._arena_offset(eng.xs[1]) is not None and eng.tp_car._arena_offset(eng.dxb[0]) is not None
     eng.load_full_params(layers)
     for x, dy in batches:
         eng.train_step(x.to(dev), dy.to(dev))
@@ -130,7 +140,7 @@ def test_tp_engine_with_custom_allreduce(free_port):
             assert (d_got - d_want).norm() / d_want.norm() < 2e-3, (l, k)
 
 
-def _stall_proc(rank, n, port, q):
+def _stall_proc(rank, n, port, q, arena=False):
     import torch.distributed as dist
 
     from dllm.parallel.car import CustomAllReduce
@@ -139,10 +149,11 @@ def _stall_proc(rank, n, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=n)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    car = CustomAllReduce(list(range(n)), dev, cap_bytes=4096 * 4, tag="stall", timeout_s=0.5)
+    car = CustomAllReduce(list(range(n)), dev, cap_bytes=4096 * 4, tag="stall", timeout_s=0.5,
+                          arena_bytes=4096 * 4 if arena else 0)
     res = None
     if rank == 0:  # rank 1 stalls: it never enters the all-reduce
-        t = torch.ones(4096, device=dev)
+        t = car.arena_view((4096,), torch.float32).fill_(1.0) if arena else torch.ones(4096, device=dev)
         car.all_reduce(t)
         try:
             car.check()
@@ -159,13 +170,14 @@ def _stall_proc(rank, n, port, q):
     q.put((rank, res))
 
 
-def test_stalled_peer_fails_loudly(free_port):
+@pytest.mark.parametrize("arena", [False, True])
+def test_stalled_peer_fails_loudly(arena, free_port):
     """A peer that never arrives: the bounded barrier times out, the result is NaN-poisoned (never a
     silently partial sum) and ``check()`` -- which the engine runs at its sync points -- raises."""
     n = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_stall_proc, args=(r, n, free_port, q)) for r in range(n)]
+    ps = [ctx.Process(target=_stall_proc, args=(r, n, free_port, q, arena)) for r in range(n)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=120) for _ in range(n))

@@ -280,3 +280,35 @@ def test_bf16_gradient_collectives_vs_fp32_oracle(method, free_port):
     init = build_params(cfg, "cpu_compat", SEED, "cpu")
     assert _update_err(got, ref_grads32, init) < 5e-2
     assert _update_err(got, _oracle(cfg, 2), init) < 0.1
+
+
+@pytest.mark.parametrize("chunks,sp,want", [(1, False, 5), (2, False, 8), (1, True, 11)])
+def test_tp_collectives_per_step_pinned(chunks, sp, want, free_port):
+    """TP collectives per step (L=3, tp=2): forward one output all-reduce per layer and chunk (the last one left in
+    flight under the backward), backward one dx all-reduce per layer except layer 0 (its input gradient is never
+    used; the reference still all-reduces it, train_ffns.py:309).  SP: per layer an input all-gather and an output
+    reduce-scatter forward, a dL/dy all-gather and (l > 0) a dx reduce-scatter backward."""
+    cfg = _cfg(D=32, F=64, L=3, T=1024, steps=2, tp_chunks=chunks, sequence_parallel=sp)
+    r = _run(cfg, 4, 2, free_port, rec=True, count_collectives=True)
+    assert r["collectives_per_step"] == {"tp": want}
+    _close(r["params"], _oracle(cfg, 1))
+
+
+def test_ddp_collectives_per_step_pinned(free_port):
+    """DDP with one bucket per weight: 2L gradient all-reduces per step (train_ffns.py:164-165)."""
+    cfg = _cfg(L=3, steps=2)
+    r = _run(cfg, 2, 2, free_port, rec=True, count_collectives=True)
+    assert r["collectives_per_step"]["dp_ar"] == 6
+
+
+@pytest.mark.parametrize("sp,want", [(False, 5), (True, 11)])
+def test_force_tp_comm_runs_tp_collectives_at_world1(sp, want, free_port):
+    """force_comm + force_tp_comm at world 1: the TP path issues its real collectives (chunked forward all-reduce,
+    deferred last-layer exchange, dx all-reduce / SP reduce-scatter + all-gathers) over the size-1 tp communicator,
+    so a one-GPU run of the MP method exercises RCCL instead of skipping the exchange; results are the single
+    device's."""
+    cfg = _cfg(D=32, F=64, L=3, T=1024, steps=2, tp_chunks=1, sequence_parallel=sp, force_comm=True,
+               force_tp_comm=True)
+    r = _run(cfg, 4, 1, free_port, rec=True, count_collectives=True, force_dist=True)
+    assert r["collectives_per_step"]["tp"] == want
+    _close(r["params"], _oracle(cfg, 1))
