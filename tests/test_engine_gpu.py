@@ -257,3 +257,50 @@ def test_wgrad_stream_bitwise(act):
         torch.cuda.synchronize()
         outs.append(eng.master.clone())
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("variant", ["8phase_stagger", "pp"])
+def test_wgrad_stream_bitwise_full_size(variant):
+    """Race screen of the bench's default schedule at a size where the two streams' grids really overlap: L4 D4096
+    F16384 T8192 bf16 (persistent 1024/512-tile GEMMs, ReLU 1-bit masks, fused SGD), 3 steps on device-generated
+    data.  The concurrent weight-gradient stream must give bitwise the serial schedule's fp32 masters."""
+    from dllm.models.ffn import init_ffn_params_device
+    from dllm.ops.gemm import set_bf16_variant
+    from dllm.utils.data import DeviceMockData
+
+    D, F, L, T = 4096, 16384, 4, 8192
+    old = set_bf16_variant(variant)
+    try:
+        outs = []
+        for ws in (False, True):
+            cfg = TrainConfig(model=ModelConfig(D, F, L, "relu", False), batch_size=8, seq_len=1024, dtype="bf16",
+                              grad_dtype="bf16", lr=1e-2, wgrad_stream=ws)
+            eng = FFNTrainer(cfg, Mesh(), torch.device("cuda"))
+            assert (eng.wg_stream is not None) == ws and eng.masks is not None
+            eng.load_full_params(init_ffn_params_device(D, F, L, 7, torch.device("cuda"), False))
+            data = DeviceMockData(T, D, torch.bfloat16, torch.device("cuda"))
+            for s in range(3):
+                x, dy = data.fill(100 + s)
+                eng.train_step(x, dy)
+            torch.cuda.synchronize()
+            outs.append(eng.master.clone())
+            del eng, data
+            torch.cuda.empty_cache()
+        assert torch.isfinite(outs[0]).all()
+        assert torch.equal(outs[0], outs[1])
+    finally:
+        set_bf16_variant(old)
+
+
+def test_sizing_plan_matches_wgrad_stream_buffers():
+    """utils/sizing.plan with wgrad_stream counts the rotated dgrad / dx buffers the engine really allocates."""
+    from dllm.utils.sizing import plan
+
+    cfg = TrainConfig(model=ModelConfig(256, 1024, 3), batch_size=2, seq_len=256, dtype="bf16", grad_dtype="bf16",
+                      lr=1e-2, wgrad_stream=True)
+    eng = FFNTrainer(cfg, Mesh(), torch.device("cuda"))
+    assert eng.wg_stream is not None
+    p = plan(256, 1024, 3, 512, dtype="bf16", grad_dtype="bf16", wgrad_stream=True)["bytes"]
+    nb = lambda t: t.numel() * t.element_size()  # noqa: E731
+    assert p["dgrad_buffer"] == sum(nb(t) for t in eng.da_ring)
+    assert p["dx_buffers"] == sum(nb(t) for t in eng.dxb)
