@@ -2,6 +2,7 @@
 // the per-layout translation units.  Kernels and launch templates: gemm_kernels.h.
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 
 #include "gemm_kernels.h"
 
@@ -33,6 +34,10 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
   a.tpb_req = tpb;
   a.min_bpc = min_bpc < 1 ? 1 : min_bpc;
   a.ws = nullptr;
+  {
+    const char* sk = getenv("DLLM_PP_SKEW");
+    a.skew = sk ? atoi(sk) : 0;
+  }
   // the LDS-DMA loads and 16-B / paired epilogue accesses of the MFMA paths need 16-B aligned bases
   const bool aligned_ptr = ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && ((uintptr_t)C % 16 == 0) &&
                            ((uintptr_t)aux % 16 == 0) && ((uintptr_t)aux_out % 16 == 0) &&

@@ -75,6 +75,9 @@ struct GemmArgs {
   // bit (act(h) != 0) per output element, EPI_DACT reads it instead of aux.  Tile-native layout: 8 KiB per
   // 256x256 tile (tile = tm * tiles_n + tn), 16 B per thread -- the same element->lane map in both GEMMs.
   void* mask;
+  // gemm_bf16_pp: initial delay (x 64 clocks) of the odd workgroup slot of each CU, so the two co-resident blocks
+  // start out of phase (experiment knob, DLLM_PP_SKEW; 0 = none)
+  int skew;
 };
 
 // ----------------------------------------------------------------------------------------------
@@ -1625,7 +1628,9 @@ static int num_cu() {
 
 // grid of a persistent 8-phase launch over nb tile slots; sets a.tpb (1: launch the one-tile kernel instead).
 // Persistent grids are a multiple of the 8 XCDs (every slot of a block maps to the block's own XCD).
-// Tiles per block t <= tpb_req, and <= ceil(nb / (ncu * min_bpc)) (blocks enough to leave CUs to collectives), chosen
+// Tiles per block t <= tpb_req, and <= ceil(nb / (ncu * min_bpc)) (blocks enough to leave CUs to collectives: the grid
+// then has ~min_bpc blocks per CU -- nb / t rounded, so e.g. 1000 tiles at min_bpc 2 run as 504 blocks of <= 2
+// tiles, 1.97 per CU; "min_bpc" bounds tiles per block, it is not a strict floor on blocks per CU), chosen
 // to minimise the makespan in tile-times, ceil(blocks / ncu) * ceil(nb / blocks) (one block per CU: 128 KiB
 // LDS); ties go to fewer blocks.  E.g. 1792 tiles on 256 CUs: 256 blocks x 7 tiles = 7 tile-times, where a
 // fixed 4 per block (448 blocks in two rounds) takes 8.

@@ -259,6 +259,13 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_pp(GemmArgs p) {
     __builtin_amdgcn_s_setprio(0);
   };
 
+  // optional skew: the odd workgroup slot of the CU (HW_ID.TG_ID) starts later, so the two co-resident blocks do
+  // not run their read / barrier / MFMA segments in lockstep
+  if (p.skew > 0) {
+    const unsigned hw = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));  // hwreg(HW_REG_HW_ID)
+    if ((hw >> 16) & 1)
+      for (int i = 0; i < p.skew; ++i) __builtin_amdgcn_s_sleep(1);
+  }
   // ring state (runs on across persistent slots): A slots of A-h0 / A-h1 of the current K-tile, B buffer parity
   int sa0 = 0, sa1 = 1, bb = 0;
   // prologue = the loads phases q1(-2) .. q3(-1) would have issued, in that order: A0(0) B0(0) B1(0) | A1(0) B0(1)

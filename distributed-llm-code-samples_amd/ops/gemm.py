@@ -343,10 +343,11 @@ def set_bf16_variant(name: str) -> str:
 
 
 def set_tiles_per_block(n: int) -> int:
-    """Persistent 8-phase GEMM blocks for the FFN's own GEMMs: each block runs up to ``n`` output tiles back to
-    back, the next tile's first K-tiles prefetched while the current tile's epilogue runs (no pipeline drain or
-    block relaunch per tile).  Capped at tiles / CUs so every CU keeps a block; ``n <= 1``: one block per tile.
-    Default 2.  Returns the previous setting."""
+    """Persistent GEMM blocks for the FFN's own GEMMs: each block runs up to ``n`` output tiles back to back, the next
+    tile's first K-tiles prefetched while the current tile's epilogue runs (no pipeline drain or block relaunch per
+    tile).  ``n`` is a cap: the launcher picks the makespan-optimal tiles per block under it (never fewer blocks than
+    CUs x ``min_bpc`` up to rounding); ``n <= 1``: one block per tile.  Default 8 (the engine's default for every
+    stack).  Returns the previous setting."""
     old = _POLICY["tpb"]
     _POLICY["tpb"] = max(1, int(n))
     return old

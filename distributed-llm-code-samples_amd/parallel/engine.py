@@ -243,6 +243,7 @@ class FFNTrainer:
             self.ag_next = set()            # layers whose post-update gather for the next forward is in flight
             self.fsdp_stream = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
             self.fsdp_tail_ev = None
+            self.fsdp_upd = {}              # layer -> event: its shard update on the side stream (backward)
 
         # ---- activations -------------------------------------------------------------------------
         Tl = T // t if self.sp else T  # tokens held per rank between layers
@@ -383,7 +384,10 @@ class FFNTrainer:
         da = self.da_ring[l % 2]
         if self.da_free[l % 2] is not None:
             main.wait_event(self.da_free[l % 2])
-        gemm(g, w2, "nn", out=da, epi="dact", act=act, aux=h if h is not None else a, mask=self._mask(l))
+        if self.gated:   # [dg|du] interleaved [T, 2F] (as layer_bwd)
+            gemm(g, w2, "nn", out=da, epi="dglu", act=act, aux=h)
+        else:
+            gemm(g, w2, "nn", out=da, epi="dact", act=act, aux=h if h is not None else a, mask=self._mask(l))
         e_da = torch.cuda.Event()
         e_da.record(main)
         side.wait_event(e_da)
@@ -685,9 +689,32 @@ class FFNTrainer:
         if not works:
             self.rs_pending[slot] = None
 
+    def _fsdp_finish_rs_side(self, slot: int) -> None:
+        """Backward: the slot's previous layer (l + 2) -- wait for its reduce-scatters on the compute stream (its
+        gradient ring slot is rewritten next) and update its shards on the side stream, off the compute stream's
+        critical path.  The next forward's gather of that layer waits for the update (``fsdp_upd``)."""
+        pend = self.rs_pending[slot]
+        if pend is None:
+            return
+        st = self.fsdp_stream
+        if st is None:
+            self._fsdp_finish_rs(slot)
+            return
+        lay, works = pend
+        for w in works.values():
+            w.wait()
+        with torch.cuda.stream(st):
+            self._fsdp_finish_rs(slot)
+            ev = torch.cuda.Event()
+            ev.record(st)
+        self.fsdp_upd[lay] = ev
+
     def _fsdp_gather(self, l: int, names=("w2", "w1")) -> None:
         slot = l % 2
         grp = self.mesh.group("dp_ag")
+        ev = self.fsdp_upd.pop(l, None)
+        if ev is not None:  # the shard was updated on the side stream
+            torch.cuda.current_stream(self.device).wait_event(ev)
         if self.ag_layer[slot] != l or self.ag_work[slot] is None:
             self.ag_work[slot] = {}
         # the weights' shard all-gathers as one group (native: one fused RCCL launch)
@@ -850,7 +877,7 @@ class FFNTrainer:
                 else:
                     w1, w2 = self._fsdp_weights(l)
                 slot = l % 2
-                self._fsdp_finish_rs(slot)  # slot's previous grads (layer l+2) must be reduced first
+                self._fsdp_finish_rs_side(slot)  # slot's previous grads (layer l+2) must be reduced first
                 gw1, gw2 = self.gring[slot]["w1"], self.gring[slot]["w2"]
             elif self.fused_opt:
                 w1, w2 = self.copy_view(l, "w1"), self.copy_view(l, "w2")
@@ -895,10 +922,11 @@ class FFNTrainer:
                     g = dx
             if self.zero:
                 # reduce-scatters issued during an earlier layer have had a full layer of compute to
-                # finish: update those shards now (1/dp of the optimizer work, off the tail)
+                # finish: update those shards now (1/dp of the optimizer work, off the tail), on the side stream
+                # so the shard update and its all-gather overlap the next GEMMs instead of running between them
                 for b, at in enumerate(self.rs_issued_at):
                     if at is not None and at > l:
-                        self._zero_finish(b)
+                        self._zero_finish(b, side=True)
 
         if self.wg_stream is not None:
             # the next forward reads the updated weights (and reuses every activation buffer)
@@ -911,11 +939,12 @@ class FFNTrainer:
                 if at is not None:
                     self._zero_finish(b, side=True)
         elif self.ddp:
-            # buckets completed before layer 0's: update on the compute stream; layer 0's (the step
-            # boundary, whose all-reduce was issued last) on the side stream, waited per weight
-            tail = set(self.weight_buckets[(0, "w1")]) | set(self.weight_buckets[(0, "w2")])
-            for b, (s, e, _) in enumerate(self.buckets):
-                if b in tail and self.opt_stream is not None:
+            # every bucket's update runs on the side stream behind its all-reduce (stream waits, no host block), in
+            # the order the next forward needs the weights (layer 0's buckets first), so the later layers' updates
+            # overlap the next forward's first GEMMs; the forward waits per weight
+            for b in reversed(range(len(self.buckets))):
+                s, e, _ = self.buckets[b]
+                if self.opt_stream is not None:
                     self.opt_stream.wait_stream(torch.cuda.current_stream(self.device))
                     with torch.cuda.stream(self.opt_stream):
                         self.bucket_work[b].wait()

@@ -72,6 +72,12 @@ class CommObserver:
     # -- lifecycle -------------------------------------------------------------------------------------
     def __enter__(self):
         global _OBS
+        # observer streams are created (and their first command retired) up front: a stream's first command runs
+        # late (measured: ~0.3 ms), which would stretch the first collective of each role
+        for role in set(self.roles.values()) | {"other"}:
+            st = self.obs_streams.setdefault(role, torch.cuda.Stream(device=self.device))
+            torch.cuda.Event(enable_timing=True).record(st)
+        torch.cuda.synchronize(self.device)
         self.t0 = torch.cuda.Event(enable_timing=True)
         self.t0.record(torch.cuda.current_stream(self.device))
         _OBS = self

@@ -88,9 +88,11 @@ def main():
                 if v.startswith("tpb"):
                     set_bf16_variant("8phase_stagger")
                     set_tiles_per_block(int(v[3:]))
-                elif v.startswith("pp"):   # 256x128 two-blocks-per-CU family; ppN: N tiles per persistent block
-                    set_bf16_variant("pp")
-                    set_tiles_per_block(int(v[2:] or 1))
+                elif v.startswith("pp"):   # 256x128 two-blocks-per-CU family; ppN[sK]: N tiles per persistent
+                    set_bf16_variant("pp")    # block, odd workgroup slot of each CU delayed K x 64 clocks
+                    tpb, _, sk = v[2:].partition("s")
+                    set_tiles_per_block(int(tpb or 1))
+                    os.environ["DLLM_PP_SKEW"] = sk or "0"
                 else:
                     set_bf16_variant(v)
                     set_tiles_per_block(1)

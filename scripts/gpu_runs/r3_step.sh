@@ -1,24 +1,14 @@
 #!/bin/bash
-# Round 3: end-to-end steps.  Flagship headline with the 256x256 8-phase family vs the 256x128 two-blocks-per-CU
-# family (interleaved, two rounds), the gated Llama-dims stack with persistent vs one-tile GEMM blocks, and the
+# Round 3: end-to-end steps: the gated Llama-dims stack with persistent vs one-tile GEMM blocks, and the
 # communicating methods at N=1 (force_comm) with the comm observer; then the observer's own known-schedule test.
 set -o pipefail
 mkdir -p gpurun_out/r3
 export PYTHONUNBUFFERED=1
-B="timeout -k 10 300 python -u bench.py --methods none --steps 20 --warmup 5"
-for r in 1 2; do
-  for v in auto pp; do
-    $B --gemm_variant $v > gpurun_out/r3/head_${v}_$r.json 2> gpurun_out/r3/head_${v}_$r.err || { tail -20 gpurun_out/r3/head_${v}_$r.err; exit 1; }
-    python -c "import json;d=json.load(open('gpurun_out/r3/head_${v}_$r.json'));print('$v', d['value'], d['ms_per_step'])"
-  done
-done
 G="timeout -k 10 300 python -u bench.py --methods none --steps 6 --warmup 2 --layers 32 --ffn_dim 14336 --gated --act silu"
 for t in 1 8; do
   $G --tpb $t > gpurun_out/r3/gated_tpb$t.json 2> gpurun_out/r3/gated_tpb$t.err || { tail -20 gpurun_out/r3/gated_tpb$t.err; exit 1; }
   python -c "import json;d=json.load(open('gpurun_out/r3/gated_tpb$t.json'));print('gated tpb$t', d['value'], d['ms_per_step'], d['tflops_per_gpu'])"
 done
-$G --tpb 8 --gemm_variant pp > gpurun_out/r3/gated_pp.json 2> gpurun_out/r3/gated_pp.err || { tail -20 gpurun_out/r3/gated_pp.err; exit 1; }
-python -c "import json;d=json.load(open('gpurun_out/r3/gated_pp.json'));print('gated pp', d['value'], d['ms_per_step'], d['tflops_per_gpu'])"
 timeout -k 10 600 python -u bench.py --steps 10 --warmup 3 --methods ddp,zero,fsdp,tp,hybrid > gpurun_out/r3/methods.json 2> gpurun_out/r3/methods.err || { tail -20 gpurun_out/r3/methods.err; exit 1; }
 python - <<'PY'
 import json

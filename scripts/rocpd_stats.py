@@ -19,6 +19,11 @@ def main():
     ap.add_argument("db")
     ap.add_argument("--last_ms", type=float, default=0.0)
     ap.add_argument("--top", type=int, default=25)
+    ap.add_argument("--overlap", default="",
+                    help="comma substrings of communication kernels (e.g. 'copyBuffer,nccl'): over the whole trace after the "
+                         "first --skip_ms, report the union of their intervals and the part under GEMM kernels "
+                         "('gemm_'), i.e. the trace's own overlap_frac to compare with the comm observer")
+    ap.add_argument("--skip_ms", type=float, default=0.0)
     ap.add_argument("--step_marker", default="",
                     help="substring of the kernel that starts a step (e.g. 'rng_normal_kernel<unsigned short>'): "
                          "print the timeline of the second-to-last complete step instead of --last_ms")
@@ -34,6 +39,34 @@ def main():
     for n, (k, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:a.top]:
         print(f"{short(n):88s} {k:6d} {t / k / 1e3:9.1f} {t / 1e6:9.2f} {100 * t / tot:6.2f}")
     print(f"total kernel time {tot / 1e6:.2f} ms over {len(rows)} dispatches")
+    if a.overlap and rows:
+        keys = a.overlap.split(",")
+        t_lo = rows[0][1] + a.skip_ms * 1e6
+        if a.last_ms > 0:  # steady state: the final window only
+            t_lo = max(t_lo, max(r[2] for r in rows) - a.last_ms * 1e6)
+
+        def union(iv):
+            out = []
+            for s_, e_ in sorted(iv):
+                if out and s_ <= out[-1][1]:
+                    out[-1][1] = max(out[-1][1], e_)
+                else:
+                    out.append([s_, e_])
+            return out
+
+        comm = union([(s_, e_) for n, s_, e_, *_ in rows if s_ >= t_lo and any(k in n for k in keys)])
+        gem = union([(s_, e_) for n, s_, e_, *_ in rows if s_ >= t_lo and "gemm_" in n])
+        hid, i, j = 0, 0, 0
+        while i < len(comm) and j < len(gem):
+            lo, hi = max(comm[i][0], gem[j][0]), min(comm[i][1], gem[j][1])
+            hid += max(0, hi - lo)
+            if comm[i][1] < gem[j][1]:
+                i += 1
+            else:
+                j += 1
+        un = sum(e_ - s_ for s_, e_ in comm)
+        print(f"\ncomm kernels {keys}: union {un / 1e6:.3f} ms, under GEMMs {hid / 1e6:.3f} ms, "
+              f"overlap_frac {hid / un if un else float('nan'):.3f}")
     win = []
     if a.step_marker and rows:
         starts = [i for i, r in enumerate(rows) if a.step_marker in r[0]]

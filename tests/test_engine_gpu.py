@@ -239,15 +239,16 @@ def test_relu_mask_engine_bitwise():
     assert torch.equal(outs[0], outs[1])
 
 
-@pytest.mark.parametrize("act", ["relu", "gelu"])
-def test_wgrad_stream_bitwise(act):
+@pytest.mark.parametrize("act,gated", [("relu", False), ("gelu", False), ("silu", True)])
+def test_wgrad_stream_bitwise(act, gated):
     """Weight-gradient GEMMs on a concurrent stream == the sequential schedule, bitwise (same kernels and
-    inputs per GEMM; the stream/event edges order every weight update after its last reader)."""
+    inputs per GEMM; the stream/event edges order every weight update after its last reader); gated (SwiGLU)
+    stacks run the DGLU dgrad on the main stream."""
     D, F, L, T, lr = 512, 2048, 4, 1024, 1e-2
-    layers, batches = _setup(D, F, L, T, act, False, 3)
+    layers, batches = _setup(D, F, L, T, act, gated, 3)
     outs = []
     for ws in (False, True):
-        cfg = TrainConfig(model=ModelConfig(D, F, L, act, False), batch_size=1, seq_len=T, dtype="bf16",
+        cfg = TrainConfig(model=ModelConfig(D, F, L, act, gated), batch_size=1, seq_len=T, dtype="bf16",
                           grad_dtype="fp32", lr=lr, wgrad_stream=ws)
         eng = FFNTrainer(cfg, Mesh(), torch.device("cuda"))
         assert (eng.wg_stream is not None) == ws

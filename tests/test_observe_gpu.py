@@ -39,12 +39,17 @@ def test_observer_overlap_known_schedule(pg, backend):
     full = torch.randn(16 << 20, device=dev, generator=g)    # 64 MiB: a size-1 reduce-scatter is one copy
     out = torch.empty_like(full)
 
+    side = torch.cuda.Stream(device=dev)
+
     def step(serial: bool):
-        w = comm.reduce_scatter_into(out, full, grp, async_op=True)
         if serial:
+            w = comm.reduce_scatter_into(out, full, grp, async_op=True)
             w.wait()          # the GEMM starts only after the collective completed
-        gemm(a, b, "nt", out=c)
-        if not serial:
+            gemm(a, b, "nt", out=c)
+        else:
+            gemm(a, b, "nt", out=c)   # the compute stream is busy ~1 ms ...
+            with torch.cuda.stream(side):  # ... while the collective is issued and runs from another stream
+                w = comm.reduce_scatter_into(out, full, grp, async_op=True)
             w.wait()
 
     for serial in (False, True):
