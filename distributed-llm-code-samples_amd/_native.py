@@ -40,6 +40,7 @@ _SIGS = {
                                c_float, c_float, c_float, c_int, c_float, c_void_p]),
     "dllm_cast": (c_int, [c_void_p, c_int, c_void_p, c_int, c_long, c_void_p]),
     "dllm_split3": (c_int, [c_void_p, c_long, c_long, c_long, c_void_p, c_int, c_int, c_void_p]),
+    "dllm_occupy": (c_int, [c_int, c_int, c_float, c_void_p, c_void_p]),
     "dllm_abi_version": (c_int, []),
 }
 _OPTIONAL_SIGS: dict = {}

@@ -228,6 +228,17 @@ __global__ __launch_bounds__(256) void split3_kernel(const float* __restrict__ s
   }
 }
 
+// Stand-in for a collective kernel's CU footprint (scripts/bench_occupancy.py): `blocks` workgroups of `threads`
+// lanes that stay resident for `ticks` of the 100 MHz s_memrealtime clock (bounded by the host at 100 ms), doing
+// only register arithmetic.  Like an RCCL channel's workgroup, a resident wave takes SIMD slots a 256-VGPR GEMM
+// block needs, so the GEMM block of that CU cannot start until it leaves.
+__global__ void occupy_kernel(long ticks, float* sink) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  float acc = (float)threadIdx.x;
+  while ((long)(__builtin_amdgcn_s_memrealtime() - t0) < ticks) acc = acc * 0.999f + 1.f;
+  if (acc == -1.f) sink[threadIdx.x] = acc;  // never true; keeps the loop
+}
+
 static inline int grid_for(long n4) {
   long g = (n4 + 255) / 256;
   if (g > 2048) g = 2048;
@@ -313,6 +324,12 @@ int dllm_split3(const float* src, long lds, long R, long C, void* dst, int role,
   int g = (int)std::min<long>((n8 + 255) / 256, 2048);
   hipLaunchKernelGGL(split3_kernel, dim3(g), dim3(256), 0, (hipStream_t)stream, src, lds, R, C, (uint16_t*)dst,
                      role, rows_form);
+  return (int)hipGetLastError();
+}
+
+int dllm_occupy(int blocks, int threads, float us, float* sink, void* stream) {
+  if (blocks <= 0 || threads <= 0 || threads > 1024 || us < 0.f || us > 1e5f) return -1;
+  hipLaunchKernelGGL(occupy_kernel, dim3(blocks), dim3(threads), 0, (hipStream_t)stream, (long)(us * 100.f), sink);
   return (int)hipGetLastError();
 }
 

@@ -153,3 +153,12 @@ def cast_(src: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:
         return dst
     dst.copy_(src.view(dst.shape) if src.shape != dst.shape else src)
     return dst
+
+
+def occupy_cus(blocks: int, us: float, threads: int = 256, device: torch.device | None = None) -> None:
+    """Keep ``blocks`` workgroups of ``threads`` lanes resident for ``us`` microseconds on the current stream: a
+    stand-in for a collective kernel's CU footprint (RCCL channels), to measure how a GEMM grid behaves when part
+    of the chip is taken (scripts/bench_occupancy.py).  Native only."""
+    dev = device or torch.device("cuda", torch.cuda.current_device())
+    rc = _native.lib().dllm_occupy(int(blocks), int(threads), float(us), None, _native.stream_ptr(dev))
+    _native.check(rc, "dllm_occupy")

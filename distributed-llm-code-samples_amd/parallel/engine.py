@@ -148,7 +148,9 @@ class FFNTrainer:
         if dev.type == "cuda":
             from ..ops.gemm import set_fp32_mode, set_min_blocks_per_cu, set_tiles_per_block
 
-            set_tiles_per_block(cfg.gemm_tiles_per_block or (1 if m.gated else 8))
+            # gated stacks too since round 3 (persistent GLU / DGLU epilogues): L32 SwiGLU 167.6 vs 168.8 ms
+            # (profiles/r3/gated_llama_dims_tpb_wgs_r3.txt)
+            set_tiles_per_block(cfg.gemm_tiles_per_block or 8)
             set_fp32_mode(cfg.fp32_gemm)
             # collectives overlapping the GEMMs (any multi-rank mesh, or forced size-1 communicators)
             set_min_blocks_per_cu(cfg.gemm_min_bpc or (2 if (mesh.world > 1 or cfg.force_comm) else 1))
