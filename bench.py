@@ -127,7 +127,9 @@ def parse(argv=None):
     p.add_argument("--wgrad_stream", action=argparse.BooleanOptionalAction, default=True,
                    help="N=1 fused path: weight-gradient GEMMs (fused SGD) on a second stream, concurrent with the "
                         "dgrads; the dispatcher fills each GEMM's tail with the other's blocks (0.5 %% faster in 5/5 "
-                        "interleaved pairs, profiles/r2/wgrad_stream_ab_r2.log); --no-wgrad_stream = serial")
+                        "interleaved pairs, profiles/r2/wgrad_stream_ab_r2.log); --no-wgrad_stream = serial.  Not for "
+                        "gated (SwiGLU) stacks: there the serial step is 1.4 %% faster (167.0 vs 169.3 ms, "
+                        "profiles/r3/gated_wgrad_stream_q16_r3.txt)")
     p.add_argument("--no_relu_mask", action="store_true",
                    help="ReLU dgrad reads the bf16 activation instead of the forward's 1-bit mask")
     p.add_argument("--fp32_gemm", choices=["bf16x6", "mfma_f32"], default="bf16x6",
@@ -199,7 +201,7 @@ def run_method(a, method: str, n: int, world: int, dev: torch.device, steps: int
                       side_optimizer=a.side_opt if headline else 0, tp_allreduce=a.tp_allreduce,
                       relu_mask=not a.no_relu_mask, gemm_tiles_per_block=a.tpb, fp32_gemm=a.fp32_gemm,
                       gemm_min_bpc=a.min_bpc,
-                      wgrad_stream=a.wgrad_stream and headline and not a.graph)
+                      wgrad_stream=a.wgrad_stream and headline and not a.graph and not a.gated)
     mesh = Mesh.build(dp, tp, force=force_comm, comm_backend="torch" if cpu else a.comm,
                       device=None if cpu else dev)
     try:

@@ -86,7 +86,18 @@ class count_collectives:
         return {r: self.counts.get(id(g), 0) for r, g in groups.items() if g is not None}
 
 
-def _issue(group, fn):
+def _group_size(group) -> int:
+    return group.size() if _native(group) else dist.get_world_size(group)
+
+
+def _moves(group, out: torch.Tensor, inp: torch.Tensor) -> bool:
+    """Whether a collective moves data: on a size-1 communicator (``force_comm`` at N=1) an in-place
+    all-reduce / all-gather / reduce-scatter launches no kernel, so the observer keeps it out of the
+    comm intervals (it still counts it)."""
+    return not (_group_size(group) == 1 and out.data_ptr() == inp.data_ptr())
+
+
+def _issue(group, fn, moves: bool = True):
     """Run ``fn()`` (which issues one collective and returns its work); with a ``CommObserver`` active the
     collective's issue and completion are recorded (utils/observe.py)."""
     if _COUNTS is not None:
@@ -96,23 +107,24 @@ def _issue(group, fn):
         return fn()
     ev = obs.issue()
     w = fn()
-    obs.issued(group, ev, w)
+    obs.issued(group, ev, w, moves=moves)
     return w
 
 
 def all_reduce(t: torch.Tensor, group, async_op: bool = True):
     if group is not None and _native(group):
-        w = _issue(group, lambda: group.all_reduce(t))
+        w = _issue(group, lambda: group.all_reduce(t), _moves(group, t, t))
         return _finish(w, async_op) if (async_op or _SERIALIZE) else (w.wait(), Done())[1]
     if not _active(group):
         return Done()
-    w = _issue(group, lambda: dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=True))
+    w = _issue(group, lambda: dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=True),
+               _moves(group, t, t))
     return _finish(w, async_op) if (async_op or _SERIALIZE) else (w.wait(), Done())[1]
 
 
 def all_gather_into(out: torch.Tensor, shard: torch.Tensor, group, async_op: bool = True):
     if group is not None and _native(group):
-        w = _issue(group, lambda: group.all_gather_into(out.view(-1), shard.reshape(-1)))
+        w = _issue(group, lambda: group.all_gather_into(out.view(-1), shard.reshape(-1)), _moves(group, out, shard))
         return _finish(w, async_op) if (async_op or _SERIALIZE) else (w.wait(), Done())[1]
     if not _active(group):
         if out.data_ptr() != shard.data_ptr():
@@ -122,13 +134,13 @@ def all_gather_into(out: torch.Tensor, shard: torch.Tensor, group, async_op: boo
     if out.numel() != shard.numel() * n:
         raise ValueError(f"all_gather_into: out {out.numel()} != {n} x shard {shard.numel()}")
     w = _issue(group, lambda: dist.all_gather_into_tensor(out.view(-1), shard.reshape(-1), group=group,
-                                                         async_op=True))
+                                                         async_op=True), _moves(group, out, shard))
     return _finish(w, async_op) if (async_op or _SERIALIZE) else (w.wait(), Done())[1]
 
 
 def reduce_scatter_into(out: torch.Tensor, full: torch.Tensor, group, async_op: bool = True):
     if group is not None and _native(group):
-        w = _issue(group, lambda: group.reduce_scatter_into(out.view(-1), full.reshape(-1)))
+        w = _issue(group, lambda: group.reduce_scatter_into(out.view(-1), full.reshape(-1)), _moves(group, out, full))
         return _finish(w, async_op) if (async_op or _SERIALIZE) else (w.wait(), Done())[1]
     if not _active(group):
         if out.data_ptr() != full.data_ptr():
@@ -138,7 +150,7 @@ def reduce_scatter_into(out: torch.Tensor, full: torch.Tensor, group, async_op: 
     if full.numel() != out.numel() * n:
         raise ValueError(f"reduce_scatter_into: full {full.numel()} != {n} x out {out.numel()}")
     w = _issue(group, lambda: dist.reduce_scatter_tensor(out.view(-1), full.reshape(-1), op=dist.ReduceOp.SUM,
-                                                        group=group, async_op=True))
+                                                        group=group, async_op=True), _moves(group, out, full))
     return _finish(w, async_op) if (async_op or _SERIALIZE) else (w.wait(), Done())[1]
 
 
@@ -161,7 +173,8 @@ def all_gather_into_many(pairs, group, async_op: bool = True):
     """All-gathers ``(out, shard)`` issued as ONE group: the native layer fuses them with
     ncclGroupStart/End (one launch, one completion event); torch / gloo issue them back to back."""
     if group is not None and _native(group) and not _SERIALIZE:
-        w = _issue(group, lambda: group.all_gather_into_many([(o.view(-1), sh.reshape(-1)) for o, sh in pairs]))
+        w = _issue(group, lambda: group.all_gather_into_many([(o.view(-1), sh.reshape(-1)) for o, sh in pairs]),
+                   any(_moves(group, o, sh) for o, sh in pairs))
         return w if async_op else (w.wait(), Done())[1]
     w = _Many([all_gather_into(o, sh, group, async_op=True) for o, sh in pairs])
     return w if async_op else (w.wait(), Done())[1]
@@ -170,7 +183,8 @@ def all_gather_into_many(pairs, group, async_op: bool = True):
 def reduce_scatter_into_many(pairs, group, async_op: bool = True):
     """Reduce-scatters ``(out, full)`` issued as ONE group (see ``all_gather_into_many``)."""
     if group is not None and _native(group) and not _SERIALIZE:
-        w = _issue(group, lambda: group.reduce_scatter_into_many([(o.view(-1), f.reshape(-1)) for o, f in pairs]))
+        w = _issue(group, lambda: group.reduce_scatter_into_many([(o.view(-1), f.reshape(-1)) for o, f in pairs]),
+                   any(_moves(group, o, f) for o, f in pairs))
         return w if async_op else (w.wait(), Done())[1]
     w = _Many([reduce_scatter_into(o, f, group, async_op=True) for o, f in pairs])
     return w if async_op else (w.wait(), Done())[1]

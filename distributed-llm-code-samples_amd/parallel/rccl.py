@@ -20,6 +20,7 @@ import torch
 import torch.distributed as dist
 
 from .. import _native
+from ..utils import observe
 
 c_int, c_long, c_void_p, c_char_p = ctypes.c_int, ctypes.c_long, ctypes.c_void_p, ctypes.c_char_p
 _PP = ctypes.POINTER(ctypes.c_void_p)
@@ -82,8 +83,9 @@ class _Event:
 class NativeWork:
     """Completion handle: ``wait()`` = current HIP stream waits on the collective's completion event."""
 
-    def __init__(self, ev: _Event, keep=()):
+    def __init__(self, ev: _Event, keep=(), span=None):
         self.ev, self.keep = ev, keep
+        self.span = span  # (start, end) timing events on the communicator stream while a CommObserver is active
 
     def wait(self):
         _check(_lib().dllm_stream_wait_event(torch.cuda.current_stream().cuda_stream, self.ev.h),
@@ -154,15 +156,27 @@ class NativeGroup:
         return self._size
 
     # -- plumbing --------------------------------------------------------------------------------------
+    def _span_event(self):
+        """Under a CommObserver: a timing event recorded on this communicator's own stream, so the observer gets
+        the collective's execution interval (after its input wait, around its kernel) instead of issue ->
+        completion as seen from other streams."""
+        if observe.active() is None:
+            return None
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(torch.cuda.ExternalStream(self.stream, device=self.device))
+        return ev
+
     def _enqueue(self, fn, keep):
         cur = torch.cuda.current_stream(self.device).cuda_stream
         ev_in = _Event()
         _check(_lib().dllm_event_record(ev_in.h, cur), "hipEventRecord")
         _check(_lib().dllm_stream_wait_event(self.stream, ev_in.h), "hipStreamWaitEvent")
+        t_s = self._span_event()
         fn(self.stream)
+        t_e = self._span_event()
         ev_out = _Event()
         _check(_lib().dllm_event_record(ev_out.h, self.stream), "hipEventRecord")
-        return NativeWork(ev_out, keep=(ev_in,) + tuple(keep))
+        return NativeWork(ev_out, keep=(ev_in,) + tuple(keep), span=(t_s, t_e) if t_s is not None else None)
 
     # -- collectives (SUM) -----------------------------------------------------------------------------
     def all_reduce(self, t: torch.Tensor) -> NativeWork:
@@ -202,6 +216,7 @@ class NativeGroup:
         ev_in = _Event()
         _check(_lib().dllm_event_record(ev_in.h, cur), "hipEventRecord")
         _check(_lib().dllm_stream_wait_event(self.stream, ev_in.h), "hipStreamWaitEvent")
+        t_s = self._span_event()
         _check(_lib().dllm_nccl_group_start(), "ncclGroupStart")
         try:
             for fn in calls:
@@ -209,9 +224,10 @@ class NativeGroup:
         finally:
             # the collectives are launched at GroupEnd, so the completion event is recorded after it
             _check(_lib().dllm_nccl_group_end(), "ncclGroupEnd")
+        t_e = self._span_event()
         ev_out = _Event()
         _check(_lib().dllm_event_record(ev_out.h, self.stream), "hipEventRecord")
-        return NativeWork(ev_out, keep=(ev_in,) + tuple(keep))
+        return NativeWork(ev_out, keep=(ev_in,) + tuple(keep), span=(t_s, t_e) if t_s is not None else None)
 
     def all_gather_into_many(self, pairs) -> NativeWork:
         """Several all-gathers ``(out, shard)`` as one group (e.g. a layer's W1 and W2 shards)."""

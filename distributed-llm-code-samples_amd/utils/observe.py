@@ -7,8 +7,14 @@ for either communicator backend (torch ProcessGroupNCCL or the native RCCL layer
 * every collective issued through ``parallel.comm`` records an *issue* event on the caller's stream, and an
   *end* event on a per-role observer stream that waits on the collective's completion (``work.wait()``
   under that stream) -- so the end timestamp is the collective's completion, whatever stream ran it;
+* the native RCCL layer (``parallel/rccl.py``) records the two events on its communicator stream itself,
+  after the input wait and after the kernel: its intervals are execution intervals, as in a kernel trace
+  (torch ProcessGroupNCCL keeps its stream private, so there the interval runs from issue to completion
+  and carries the launch / event latency: ~20-30 us per collective);
 * a collective queued behind an earlier one of its role cannot start before that one ends, so its start is
   ``max(issue, previous end of the role)`` (one communicator = one stream per role);
+* a collective that moves no data (in place on a size-1 communicator: ``force_comm`` at N=1) launches no
+  kernel; it is counted but kept out of the intervals, as a kernel trace of the same run has nothing for it;
 * every native GEMM records events around its launch on the compute stream (``ops.gemm`` calls
   ``gemm_begin`` / ``gemm_end``); the start event fires when the GEMM can start (after any stream wait).
 
@@ -64,6 +70,7 @@ class CommObserver:
         self.roles = {id(g): r for r, g in (roles or {}).items() if g is not None}
         self.obs_streams: dict[str, torch.cuda.Stream] = {}
         self.colls: list[tuple[str, torch.cuda.Event, torch.cuda.Event]] = []
+        self.n_noop = 0  # collectives that moved no data (counted, no interval)
         self.gemms: list[tuple[torch.cuda.Event, torch.cuda.Event]] = []
         self._open: torch.cuda.Event | None = None
         self.t0: torch.cuda.Event | None = None
@@ -97,8 +104,15 @@ class CommObserver:
         ev.record(torch.cuda.current_stream(self.device))
         return ev
 
-    def issued(self, group, ev_issue: torch.cuda.Event, work) -> None:
+    def issued(self, group, ev_issue: torch.cuda.Event, work, moves: bool = True) -> None:
+        if not moves:
+            self.n_noop += 1
+            return
         role = self.role_of(group)
+        span = getattr(work, "span", None)
+        if span is not None:  # native communicator: timing events on its own stream around the kernel
+            self.colls.append((role, span[0], span[1]))
+            return
         st = self.obs_streams.get(role)
         if st is None:
             st = self.obs_streams[role] = torch.cuda.Stream(device=self.device)
@@ -144,7 +158,8 @@ class CommObserver:
         return {
             "comm_ms": round(union_ms / steps, 3),
             "comm_ms_by_role": {r: round(_length(_union(iv)) / steps, 3) for r, iv in sorted(per_role.items())},
-            "collectives_per_step": round(len(self.colls) / steps, 1),
+            "collectives_per_step": round((len(self.colls) + self.n_noop) / steps, 1),
+            "noop_collectives_per_step": round(self.n_noop / steps, 1),
             "comm_hidden_ms": round(hidden / steps, 3),
             "comm_exposed_ms": round((union_ms - hidden) / steps, 3),
             "overlap_frac": round(hidden / union_ms, 4) if union_ms > 0 else None,

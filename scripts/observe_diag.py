@@ -3,6 +3,11 @@ CommObserver and print the raw intervals of the last step (collective issue -> c
 end) next to the summary, so the observer's overlap can be checked against a rocprofv3 trace of the same run.
 
     python scripts/observe_diag.py --method zero [--steps 3] [--layers 8]
+
+Same-run check against the kernel trace (scripts/gpu_runs/r3_obs.sh):
+    rocprofv3 --kernel-trace -d gpurun_out/obs_zero -o run -- python3 scripts/observe_diag.py --method zero
+    python scripts/rocpd_stats.py gpurun_out/obs_zero/run_results.db --overlap copyBuffer,nccl,rccl \
+        --step_marker 'rng_normal_kernel<unsigned short>' --from_marker 3
 """
 import argparse
 import json

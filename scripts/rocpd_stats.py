@@ -24,6 +24,9 @@ def main():
                          "first --skip_ms, report the union of their intervals and the part under GEMM kernels "
                          "('gemm_'), i.e. the trace's own overlap_frac to compare with the comm observer")
     ap.add_argument("--skip_ms", type=float, default=0.0)
+    ap.add_argument("--from_marker", type=int, default=0,
+                    help="--overlap window starts at the K-th last step start (--step_marker, draws 2 per step): "
+                         "the window a CommObserver over the last K steps of the same process saw")
     ap.add_argument("--step_marker", default="",
                     help="substring of the kernel that starts a step (e.g. 'rng_normal_kernel<unsigned short>'): "
                          "print the timeline of the second-to-last complete step instead of --last_ms")
@@ -44,6 +47,9 @@ def main():
         t_lo = rows[0][1] + a.skip_ms * 1e6
         if a.last_ms > 0:  # steady state: the final window only
             t_lo = max(t_lo, max(r[2] for r in rows) - a.last_ms * 1e6)
+        if a.from_marker and a.step_marker:
+            starts = [r[1] for r in rows if a.step_marker in r[0]][::2]
+            t_lo = max(t_lo, starts[-a.from_marker])
 
         def union(iv):
             out = []

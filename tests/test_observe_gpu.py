@@ -68,3 +68,23 @@ def test_observer_overlap_known_schedule(pg, backend):
     assert res[False]["overlap_frac"] >= 0.8, res
     assert res[True]["overlap_frac"] <= 0.2, res
     mesh.destroy()
+
+
+@pytest.mark.parametrize("backend", ["torch", "native"])
+def test_observer_skips_collectives_that_move_nothing(pg, backend):
+    """On a size-1 communicator an in-place all-reduce / all-gather launches no kernel: counted, no interval;
+    an out-of-place one is a copy and gets an interval."""
+    dev = torch.device("cuda", 0)
+    mesh = Mesh.build(1, 1, force=True, comm_backend=backend, device=dev)
+    grp = mesh.group("dp_ag")
+    t = torch.randn(4 << 20, device=dev)
+    o = torch.empty_like(t)
+    with CommObserver(dev, dict(mesh.groups)) as obs:
+        comm.all_reduce(t, grp).wait()
+        comm.all_gather_into(t, t, grp).wait()
+        comm.all_gather_into(o, t, grp).wait()
+    s = obs.summary(1)
+    assert s["collectives_per_step"] == 3.0 and s["noop_collectives_per_step"] == 2.0, s
+    assert len(obs.colls) == 1 and s["comm_ms"] > 0.0, s
+    assert torch.equal(o, t)
+    mesh.destroy()
