@@ -36,7 +36,7 @@ def _proc(rank, n, port, numel, dtype, q, arena=False):
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     car = CustomAllReduce(list(range(n)), dev, cap_bytes=numel * 4, tag="test",
-                          arena_bytes=2 * numel * 4 if arena else 0)
+                          arena_bytes=2 * (numel * 4 + 256) if arena else 0)  # views are 256-B aligned
     # arena: two tensors carved from the zero-copy arena (the second at a non-zero offset), all-reduced in place
     views = [car.arena_view((numel,), dtype) for _ in range(2)] if arena else None
     ok = True

@@ -275,10 +275,11 @@ def test_wgrad_stream_bitwise_full_size(variant):
         outs = []
         for ws in (False, True):
             cfg = TrainConfig(model=ModelConfig(D, F, L, "relu", False), batch_size=8, seq_len=1024, dtype="bf16",
-                              grad_dtype="bf16", lr=1e-2, wgrad_stream=ws)
+                              grad_dtype="bf16", wgrad_stream=ws)   # the bench's lr: lr 1e-2 overflows
             eng = FFNTrainer(cfg, Mesh(), torch.device("cuda"))
             assert (eng.wg_stream is not None) == ws and eng.masks is not None
             eng.load_full_params(init_ffn_params_device(D, F, L, 7, torch.device("cuda"), False))
+            init_master = eng.master.clone()
             data = DeviceMockData(T, D, torch.bfloat16, torch.device("cuda"))
             for s in range(3):
                 x, dy = data.fill(100 + s)
@@ -288,6 +289,7 @@ def test_wgrad_stream_bitwise_full_size(variant):
             del eng, data
             torch.cuda.empty_cache()
         assert torch.isfinite(outs[0]).all()
+        assert not torch.equal(outs[0], init_master), "the steps must move the masters"
         assert torch.equal(outs[0], outs[1])
     finally:
         set_bf16_variant(old)
