@@ -130,6 +130,9 @@ def parse(argv=None):
                         "interleaved pairs, profiles/r2/wgrad_stream_ab_r2.log); --no-wgrad_stream = serial.  Not for "
                         "gated (SwiGLU) stacks: there the serial step is 1.4 %% faster (167.0 vs 169.3 ms, "
                         "profiles/r3/gated_wgrad_stream_q16_r3.txt)")
+    p.add_argument("--no_data_overlap", action="store_true",
+                   help="draw each step's batch on the compute stream at the start of the step (default: the next "
+                        "batch is drawn on a side stream under the current backward)")
     p.add_argument("--no_relu_mask", action="store_true",
                    help="ReLU dgrad reads the bf16 activation instead of the forward's 1-bit mask")
     p.add_argument("--fp32_gemm", choices=["bf16x6", "mfma_f32"], default="bf16x6",
@@ -228,7 +231,8 @@ def _run_on_mesh(a, method, cfg, mesh, n, world, dev, steps, warmup, force_comm,
     eng.load_full_params(init_ffn_params_device(model.D, model.F, model.layers, a.seed, dev, model.gated,
                                                 scale=init_scale))
     sync()
-    data = DeviceMockData(cfg.tokens, model.D, cfg.torch_dtype, dev)
+    # one-deep data pipeline: step s+1's batch is drawn on a side stream under step s's backward
+    data = DeviceMockData(cfg.tokens, model.D, cfg.torch_dtype, dev, overlap=not a.no_data_overlap and not a.graph)
     seed_base = 10_000 * (mesh.dp_rank + 1)
 
     graphed = None
@@ -236,12 +240,14 @@ def _run_on_mesh(a, method, cfg, mesh, n, world, dev, steps, warmup, force_comm,
         from dllm.utils.graphs import GraphedStep
 
         graphed = GraphedStep(eng, cfg.tokens, model.D)
+    else:
+        eng.before_backward = data.release
 
     def one_step(seed):
         if graphed is not None:
             graphed.step(seed)
         else:
-            x, dy = data.fill(seed)
+            x, dy = data.fill(seed, next_seed=seed + 1)
             eng.train_step(x, dy)
 
     for i in range(warmup):
@@ -329,7 +335,9 @@ def main(argv=None) -> int:
             "metric": METRIC, "value": head["value"], "unit": "tokens/s", "n_gpus": 0 if cpu else n,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": head["ms_per_step"], "higher_is_better": True,
             "scaling": "strong" if a.method == "tp" else "weak", "vs_baseline": None, "dtype": a.dtype,
-            "data": "synthetic (device Philox N(0,1) x, 0.1*N(0,1) dloss/dx; random-init weights)",
+            "data": "synthetic (device Philox N(0,1) x, 0.1*N(0,1) dloss/dx, drawn every step" +
+                    ("" if a.no_data_overlap else ", the next batch on a side stream under the backward") +
+                    "; random-init weights)",
             "config": {"model": head["model"], "global_batch": head["global_batch"], "seq_len": a.seq_len,
                        "parallelism": head["parallelism"], "optimizer": a.optimizer, "grad_dtype": a.grad_dtype,
                        "master_weights": "fp32"},

@@ -300,6 +300,7 @@ class FFNTrainer:
                 if relu_mask_supported(T // c, self.F_loc, D, self.cd):
                     self.sp_chunks = c
         self._tp_pending = None
+        self.before_backward = None  # optional callable at the start of every backward (data pipelines)
         # concurrent weight-gradient stream (single device, fused optimizer, kept activations): the dgrad
         # chain (da, dx) stays on the compute stream, dW2 / dW1 run on a side stream after the dgrad that
         # last reads the weight they update; da / dx buffers rotate so the side stream's reads never race
@@ -860,6 +861,8 @@ class FFNTrainer:
         self._unmark(mark)
         # ---------------- backward ----------------
         mark = self._mark("backward")
+        if self.before_backward is not None:
+            self.before_backward()  # e.g. the data pipeline starts drawing the next batch (utils/data.py)
         self._next_bucket = 0
         if self.fsdp and self.fsdp_tail_ev is not None:
             # the previous step's tail reduce-scatters read the gradient ring this backward rewrites

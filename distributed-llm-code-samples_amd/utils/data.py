@@ -25,19 +25,62 @@ def reference_mock_data(seeds, batch_size: int, model_size: int):
 
 
 class DeviceMockData:
-    def __init__(self, tokens: int, model_size: int, dtype: torch.dtype, device: torch.device):
+    """Device-generated batches.  ``overlap=True`` (GPU) turns it into a one-deep data pipeline: two batch slots,
+    and the next step's batch is drawn on a side stream while the current step's backward runs -- the engine
+    calls ``release()`` at the start of its backward (``FFNTrainer.before_backward``); the next ``fill`` makes
+    the compute stream wait for that draw only.  The slot being drawn into was last read by the previous step,
+    which the compute stream has finished by then (stream order, and the weight-gradient stream is joined at
+    the end of every step).  Values are identical to the synchronous mode (same seeds, same kernel)."""
+
+    def __init__(self, tokens: int, model_size: int, dtype: torch.dtype, device: torch.device,
+                 overlap: bool = False):
         self.x = torch.empty((tokens, model_size), dtype=dtype, device=device)
         self.dy = torch.empty((tokens, model_size), dtype=dtype, device=device)
-
-    depth = 0  # device generation needs no prefetch
+        self.overlap = bool(overlap) and torch.device(device).type == "cuda"
+        self.depth = 1 if self.overlap else 0  # how far ahead callers name next_seed (0: no prefetch)
+        if self.overlap:
+            self._slots = [(self.x, self.dy), (torch.empty_like(self.x), torch.empty_like(self.dy))]
+            self._stream = torch.cuda.Stream(device=device)
+            self._n = 0
+            self._pending = None  # (seed, slot) to draw at the next release()
+            self._ready = None    # (seed, slot, event) drawn ahead
 
     def prefetch(self, seed: int) -> None:
         return None
 
+    @staticmethod
+    def _draw(x: torch.Tensor, dy: torch.Tensor, seed: int) -> None:
+        rng_normal_(x, seed=int(seed), stream_id=STREAM_X, scale=1.0)
+        rng_normal_(dy, seed=int(seed), stream_id=STREAM_DY, scale=DLOSS_DX_COEF)
+
     def fill(self, seed: int, next_seed: int | None = None) -> tuple[torch.Tensor, torch.Tensor]:
-        rng_normal_(self.x, seed=int(seed), stream_id=STREAM_X, scale=1.0)
-        rng_normal_(self.dy, seed=int(seed), stream_id=STREAM_DY, scale=DLOSS_DX_COEF)
-        return self.x, self.dy
+        if not self.overlap:
+            self._draw(self.x, self.dy, seed)
+            return self.x, self.dy
+        k = self._n % 2
+        self._n += 1
+        if self._ready is not None and self._ready[:2] == (int(seed), k):
+            torch.cuda.current_stream(self.x.device).wait_event(self._ready[2])
+        else:
+            self._draw(*self._slots[k], seed)
+        self._ready = None
+        self._pending = (int(next_seed), k ^ 1) if next_seed is not None else None
+        return self._slots[k]
+
+    def release(self) -> None:
+        """Start drawing the announced next batch on the side stream (after everything issued so far)."""
+        if not self.overlap or self._pending is None:
+            return
+        seed, k = self._pending
+        self._pending = None
+        go = torch.cuda.Event()
+        go.record(torch.cuda.current_stream(self.x.device))
+        self._stream.wait_event(go)
+        with torch.cuda.stream(self._stream):
+            self._draw(*self._slots[k], seed)
+            done = torch.cuda.Event()
+            done.record(self._stream)
+        self._ready = (seed, k, done)
 
 
 class CpuCompatData:

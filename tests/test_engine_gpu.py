@@ -307,3 +307,28 @@ def test_sizing_plan_matches_wgrad_stream_buffers():
     nb = lambda t: t.numel() * t.element_size()  # noqa: E731
     assert p["dgrad_buffer"] == sum(nb(t) for t in eng.da_ring)
     assert p["dx_buffers"] == sum(nb(t) for t in eng.dxb)
+
+
+def test_overlapped_data_pipeline_bitwise():
+    """The bench's one-deep data pipeline (next batch drawn on a side stream under the backward) gives bitwise the
+    masters of drawing each batch at the start of its step, with the wgrad stream on."""
+    from dllm.models.ffn import init_ffn_params_device
+    from dllm.utils.data import DeviceMockData
+
+    D, F, L, T = 512, 2048, 3, 2048
+    outs = []
+    for overlap in (False, True):
+        cfg = TrainConfig(model=ModelConfig(D, F, L, "relu", False), batch_size=2, seq_len=1024, dtype="bf16",
+                          grad_dtype="bf16", wgrad_stream=True)
+        eng = FFNTrainer(cfg, Mesh(), torch.device("cuda"))
+        eng.load_full_params(init_ffn_params_device(D, F, L, 3, torch.device("cuda"), False))
+        data = DeviceMockData(T, D, torch.bfloat16, torch.device("cuda"), overlap=overlap)
+        assert data.overlap == overlap
+        eng.before_backward = data.release
+        for s in range(5):
+            x, dy = data.fill(50 + s, next_seed=51 + s)
+            eng.train_step(x, dy)
+        torch.cuda.synchronize()
+        outs.append(eng.master.clone())
+    assert torch.isfinite(outs[0]).all()
+    assert torch.equal(outs[0], outs[1])
