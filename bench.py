@@ -130,9 +130,11 @@ def parse(argv=None):
                         "interleaved pairs, profiles/r2/wgrad_stream_ab_r2.log); --no-wgrad_stream = serial.  Not for "
                         "gated (SwiGLU) stacks: there the serial step is 1.4 %% faster (167.0 vs 169.3 ms, "
                         "profiles/r3/gated_wgrad_stream_q16_r3.txt)")
-    p.add_argument("--no_data_overlap", action="store_true",
-                   help="draw each step's batch on the compute stream at the start of the step (default: the next "
-                        "batch is drawn on a side stream under the current backward)")
+    p.add_argument("--data_overlap", action="store_true",
+                   help="one-deep data pipeline: draw the next step's batch on a side stream under the current "
+                        "backward (default: each batch on the compute stream at the start of its step).  The draw "
+                        "co-runs with a backward GEMM and slows it: L8 flagship 30.18 / 30.63 vs 30.12 / 29.99 ms, "
+                        "TP8 shard 0.630 vs 0.640 ms (profiles/r3/data_overlap_r3.txt)")
     p.add_argument("--no_relu_mask", action="store_true",
                    help="ReLU dgrad reads the bf16 activation instead of the forward's 1-bit mask")
     p.add_argument("--fp32_gemm", choices=["bf16x6", "mfma_f32"], default="bf16x6",
@@ -231,8 +233,8 @@ def _run_on_mesh(a, method, cfg, mesh, n, world, dev, steps, warmup, force_comm,
     eng.load_full_params(init_ffn_params_device(model.D, model.F, model.layers, a.seed, dev, model.gated,
                                                 scale=init_scale))
     sync()
-    # one-deep data pipeline: step s+1's batch is drawn on a side stream under step s's backward
-    data = DeviceMockData(cfg.tokens, model.D, cfg.torch_dtype, dev, overlap=not a.no_data_overlap and not a.graph)
+    # --data_overlap: one-deep data pipeline, step s+1's batch drawn on a side stream under step s's backward
+    data = DeviceMockData(cfg.tokens, model.D, cfg.torch_dtype, dev, overlap=a.data_overlap and not a.graph)
     seed_base = 10_000 * (mesh.dp_rank + 1)
 
     graphed = None
@@ -336,7 +338,7 @@ def main(argv=None) -> int:
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": head["ms_per_step"], "higher_is_better": True,
             "scaling": "strong" if a.method == "tp" else "weak", "vs_baseline": None, "dtype": a.dtype,
             "data": "synthetic (device Philox N(0,1) x, 0.1*N(0,1) dloss/dx, drawn every step" +
-                    ("" if a.no_data_overlap else ", the next batch on a side stream under the backward") +
+                    (", the next batch on a side stream under the backward" if a.data_overlap else "") +
                     "; random-init weights)",
             "config": {"model": head["model"], "global_batch": head["global_batch"], "seq_len": a.seq_len,
                        "parallelism": head["parallelism"], "optimizer": a.optimizer, "grad_dtype": a.grad_dtype,
