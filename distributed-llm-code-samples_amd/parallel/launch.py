@@ -66,7 +66,9 @@ def run_rank(rank: int, world: int, cfg_dict: dict, method: int, backend: str, p
     from .mesh import Mesh, init_distributed
 
     cfg = _cfg_from_dict(cfg_dict)
-    use_gpu = backend == "nccl"
+    # opts["device"] == "cuda" with gloo: several ranks share one GPU (RCCL refuses two ranks on one device), so
+    # the multi-rank engine paths run with the HIP kernels and streams, collectives staged through the host
+    use_gpu = backend == "nccl" or opts.get("device") == "cuda"
     if world > 1 or opts.get("force_dist"):
         init_distributed(backend, rank, world, "127.0.0.1", port)
     device = torch.device("cuda", torch.cuda.current_device()) if use_gpu else torch.device("cpu")
