@@ -60,14 +60,14 @@ def test_fp32_methods_match_oracle(method, n, opts, free_port):
 def test_bf16_data_parallel_methods_agree(free_port):
     """bf16 compute and bf16 gradient collectives (the bench's N > 1 path) at a size that runs the 8-phase
     persistent kernels with ReLU masks: DDP (all-reduce), ZeRO-2 (reduce-scatter, sharded update, all-gather)
-    and FSDP (gathered weights) on 2 ranks sum the same two bf16 gradients, so their masters agree."""
+    and FSDP (gathered weights) on 2 ranks sum the same two bf16 gradients, so their masters are equal."""
     cfg = _cfg(1024, 4096, 2, 2048, dtype="bf16", grad_dtype="bf16", lr=1e-3)
     ddp = _run(cfg, 2, 2, free_port)
     zero = _run(cfg, 6, 2, free_port + 1)
     fsdp = _run(cfg, 3, 2, free_port + 2)
-    for other in (zero, fsdp):
-        _close(other, ddp, rtol=2e-2, atol=1e-5)
-    print("ddp==zero bitwise:", _equal(ddp, zero), "ddp==fsdp bitwise:", _equal(ddp, fsdp))
+    # two-rank sums are order-free and every update is the same elementwise kernel: bitwise equal
+    # (profiles/r3/pytest_multirank_gpu_r3.txt)
+    assert _equal(ddp, zero) and _equal(ddp, fsdp)
 
 
 @pytest.mark.parametrize("method", [6, 3], ids=["zero2", "fsdp"])
