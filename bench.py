@@ -104,8 +104,10 @@ def parse(argv=None):
     p.add_argument("--json_out", default="")
     p.add_argument("--comm", choices=["torch", "native"], default="torch",
                    help="role communicators: torch ProcessGroupNCCL or the native C++ RCCL layer")
-    p.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
-                   help="gloo = CPU dry run of the multi-rank path (tests; tiny dims)")
+    p.add_argument("--backend", choices=["nccl", "gloo", "gloo_gpu"], default="nccl",
+                   help="gloo = CPU dry run of the multi-rank path (tests; tiny dims); gloo_gpu = the N-rank path "
+                        "with the HIP kernels on the GPU(s) and gloo collectives on device tensors, so N ranks may "
+                        "share one GPU (RCCL refuses that): a plumbing rehearsal of the N>1 bench, not a measurement")
     p.add_argument("--graph", action="store_true",
                    help="capture the whole step (data + fwd + bwd + fused SGD) in a HIP graph (N=1 path)")
     p.add_argument("--side_opt", type=int, default=0,
@@ -314,12 +316,12 @@ def main(argv=None) -> int:
         raise SystemExit(f"--gpus {n} but WORLD_SIZE={world}: launch N>1 with torchrun")
     cpu = a.backend == "gloo"
     methods = [m for m in a.methods.split(",") if m and m != "none"]
+    if not cpu:
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count()))
     if world > 1 or a.force_comm or methods:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
-        init_distributed(a.backend)
-    elif not cpu:
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        init_distributed("gloo" if a.backend == "gloo_gpu" else a.backend)
     dev = torch.device("cpu") if cpu else torch.device("cuda", torch.cuda.current_device())
     if a.gemm_variant != "auto" and not cpu:
         from dllm.ops.gemm import set_bf16_variant
@@ -362,6 +364,9 @@ def main(argv=None) -> int:
             rec["note"] = "force_comm: headline collectives over size-1 RCCL communicators"
         if cpu:
             rec["note"] = f"CPU/gloo dry run with {world} ranks (plumbing only, not a measurement)"
+        elif a.backend == "gloo_gpu":
+            rec["note"] = (f"gloo_gpu rehearsal: {world} ranks on {torch.cuda.device_count()} GPU(s), gloo collectives "
+                           "through the host (plumbing only, not a measurement)")
         if note:
             rec["note"] = (rec.get("note", "") + "; " + note).lstrip("; ")
         return rec
