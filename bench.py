@@ -119,7 +119,7 @@ def parse(argv=None):
                    help="TP activation all-reduce: RCCL, or the custom two-shot xGMI peer all-reduce (csrc/car.hip)")
     p.add_argument("--gemm_variant", default="auto",
                    choices=["auto", "2stage", "8phase", "8phase_stagger", "4phase_stagger", "pp"],
-                   help="bf16 GEMM main-loop schedule (auto = 8-phase staggered when K % 128 == 0; pp = 256x128 tiles, "
+                   help="bf16 GEMM main-loop schedule (auto = 8-phase staggered when K %% 128 == 0; pp = 256x128 tiles, "
                         "two blocks per CU)")
     p.add_argument("--tpb", type=int, default=0,
                    help="cap on tiles per persistent GEMM block (0 = auto: 8, the launcher picks the makespan-optimal "
@@ -141,6 +141,12 @@ def parse(argv=None):
                    help="ReLU dgrad reads the bf16 activation instead of the forward's 1-bit mask")
     p.add_argument("--fp32_gemm", choices=["bf16x6", "mfma_f32"], default="bf16x6",
                    help="--dtype fp32 GEMMs: exact 3-way bf16 split on the bf16 MFMA kernels, or the fp32 MFMA kernel")
+    p.add_argument("--master", choices=["split", "fp32"], default="split",
+                   help="fp32 master weights of a bf16 SGD run: split (bf16 working copy + int16 residual, exactly the "
+                        "fp32 master, 4 B/param) or a separate fp32 buffer (6 B/param with the copy)")
+    p.add_argument("--no_splitk_seam", action="store_true",
+                   help="split-K GEMMs (small tile grids, e.g. TP shards): a separate splitk_reduce pass instead of the "
+                        "in-kernel combine")
     p.add_argument("--force_comm", action="store_true",
                    help="exercise the RCCL DDP/FSDP path of the headline at N=1 (size-1 communicators)")
     return p.parse_args(argv)
@@ -170,7 +176,8 @@ def model_name(m: ModelConfig) -> str:
 def state_gib(eng) -> dict:
     """Per-rank persistent training state (GiB): fp32 master (+ optimizer moments), compute copy, grads."""
     g = lambda t: round(t.numel() * t.element_size() / 2**30, 3)  # noqa: E731
-    out = {"master_fp32": g(eng.master), "compute_copy": 0.0 if eng.shared_copy else g(eng.copy),
+    key = "master_residual" if eng.split else "master_fp32"  # split: the fp32 master = working copy + int16 plane
+    out = {key: round(eng.master_bytes / 2**30, 3), "compute_copy": 0.0 if eng.shared_copy else g(eng.copy),
            "grads": g(eng.grads)}
     if getattr(eng, "adam_m", None) is not None:
         out["adam_mv"] = round(2 * g(eng.adam_m), 3)
@@ -207,7 +214,7 @@ def run_method(a, method: str, n: int, world: int, dev: torch.device, steps: int
                       force_tp_comm=force_comm and method in ("tp", "hybrid"),
                       side_optimizer=a.side_opt if headline else 0, tp_allreduce=a.tp_allreduce,
                       relu_mask=not a.no_relu_mask, gemm_tiles_per_block=a.tpb, fp32_gemm=a.fp32_gemm,
-                      gemm_min_bpc=a.min_bpc,
+                      gemm_min_bpc=a.min_bpc, master=a.master,
                       wgrad_stream=a.wgrad_stream and headline and not a.graph and not a.gated)
     mesh = Mesh.build(dp, tp, force=force_comm, comm_backend="torch" if cpu else a.comm,
                       device=None if cpu else dev)
@@ -278,7 +285,8 @@ def _run_on_mesh(a, method, cfg, mesh, n, world, dev, steps, warmup, force_comm,
     rec = {"value": round(cfg.tokens * dp * steps / el, 1), "ms_per_step": round(ms, 3),
            "tflops_per_gpu": round(flops_per_step(cfg, tp=tp, recompute=cfg.recompute) / (ms / 1e3) / 1e12, 1),
            "peak_hbm_gib": 0.0 if cpu else round(torch.cuda.max_memory_allocated(dev) / 2**30, 2),
-           "finite": bool(torch.isfinite(eng.master[:1024]).all().item()),
+           "finite": bool(torch.isfinite(eng.master_slice(0, 1024)).all().item()),
+           "master": "fp32 (split: bf16 working copy + int16 residual)" if eng.split else "fp32",
            "global_batch": a.batch_size * dp, "parallelism": parallelism(method, n, dp, tp, world, force_comm),
            "model": model_name(model), "steps": steps, "warmup": warmup, "state_gib": state_gib(eng),
            "wgrad_stream": eng.wg_stream is not None}
@@ -327,6 +335,10 @@ def main(argv=None) -> int:
         from dllm.ops.gemm import set_bf16_variant
 
         set_bf16_variant(a.gemm_variant)
+    if a.no_splitk_seam and not cpu:
+        from dllm.ops.gemm import set_splitk_seam
+
+        set_splitk_seam(False)
     ffn = a.ffn_dim or (a.mp_ffn_dim if a.method == "tp" else 0)
     model = ModelConfig(model_size=a.model_size, ffn_dim=ffn, layers=a.layers, act=a.act, gated=a.gated)
     head = run_method(a, a.method, n, world, dev, a.steps, a.warmup, a.force_comm, model,
@@ -344,7 +356,7 @@ def main(argv=None) -> int:
                     "; random-init weights)",
             "config": {"model": head["model"], "global_batch": head["global_batch"], "seq_len": a.seq_len,
                        "parallelism": head["parallelism"], "optimizer": a.optimizer, "grad_dtype": a.grad_dtype,
-                       "master_weights": "fp32"},
+                       "master_weights": head.get("master", "fp32")},
             "tflops_per_gpu": head["tflops_per_gpu"],
             "mfu_dense": round(head["tflops_per_gpu"] / peak_tflops(a.dtype, a.fp32_gemm), 4),
             "peak_hbm_gib": head["peak_hbm_gib"], "state_gib": head["state_gib"], "finite": head["finite"],

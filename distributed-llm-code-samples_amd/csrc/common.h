@@ -28,7 +28,10 @@ enum Layout : int { L_NT = 0, L_NN = 1, L_TN = 2 };
 //   EPI_SGD   : weight-gradient GEMM fused with the SGD update: C (fp32 master) += -lr*alpha*acc,
 //               aux_out (bf16 working copy, nullable) = bf16(C)   (train_ffns.py:114,172 fused)
 //   EPI_ADAM  : same with AdamW (moments m/v share C's layout)
-enum Epi : int { EPI_STORE = 0, EPI_ACT = 1, EPI_DACT = 2, EPI_GLU = 3, EPI_DGLU = 4, EPI_SGD = 5, EPI_ADAM = 6 };
+//   EPI_SGDS  : EPI_SGD on a split master (below): C = the 16-bit residual plane, aux_out = the bf16 working copy
+//               (required); reads 4 B and writes 4 B per parameter instead of reading 4 B and writing 6 B
+enum Epi : int { EPI_STORE = 0, EPI_ACT = 1, EPI_DACT = 2, EPI_GLU = 3, EPI_DGLU = 4, EPI_SGD = 5, EPI_ADAM = 6,
+                 EPI_SGDS = 7 };
 enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_SILU = 2, ACT_GELU = 3 };
 
 __device__ __forceinline__ float bf2f(uint16_t v) {
@@ -38,6 +41,31 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   // plain cast -> v_cvt_pk_bf16_f32 (RNE, NaN-preserving) on gfx950
   __bf16 b = (__bf16)f;
   return __builtin_bit_cast(uint16_t, b);
+}
+
+// Split fp32 master weights.  The fp32 master w is stored as two 16-bit planes: hi = its bf16 working copy (the
+// GEMM operand), rounded half away from zero, and lo = the signed residual, so that
+//   bits(w) = (hi << 16) + sext(lo)      (mod 2^32; lossless for every bit pattern)
+// with t = bits(w) + 0x8000: hi = t >> 16, lo = (t & 0xffff) ^ 0x8000.  The master stays exactly the fp32 value
+// the unsplit update computes; only the working copy's rounding differs from RNE, on exact ties.  (A NaN with
+// payload bits >= 0xffff8000 keeps its master bits but gets hi = +0.)  Word forms: two elements per 32-bit word,
+// element 0 in bits 0-15.
+__device__ __forceinline__ void split_join2(uint32_t wh, uint32_t wl, float& f0, float& f1) {
+  f0 = __uint_as_float((wh << 16) + (uint32_t)((int32_t)(wl << 16) >> 16));
+  f1 = __uint_as_float((wh & 0xffff0000u) + (uint32_t)((int32_t)wl >> 16));
+}
+__device__ __forceinline__ void split_part2(float f0, float f1, uint32_t& wh, uint32_t& wl) {
+  const uint32_t t0 = __float_as_uint(f0) + 0x8000u, t1 = __float_as_uint(f1) + 0x8000u;
+  wh = (t0 >> 16) | (t1 & 0xffff0000u);
+  wl = ((t0 ^ 0x8000u) & 0xffffu) | ((t1 ^ 0x8000u) << 16);
+}
+__device__ __forceinline__ float split_join(uint16_t h, uint16_t l) {
+  return __uint_as_float(((uint32_t)h << 16) + (uint32_t)(int32_t)(int16_t)l);
+}
+__device__ __forceinline__ void split_part(float f, uint16_t& h, uint16_t& l) {
+  const uint32_t t = __float_as_uint(f) + 0x8000u;
+  h = (uint16_t)(t >> 16);
+  l = (uint16_t)((t ^ 0x8000u) & 0xffffu);
 }
 
 __device__ __forceinline__ float act_fwd(int act, float x) {

@@ -101,6 +101,36 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* master, const void* gra
   }
 }
 
+// SGD on a split master (common.h split_join2 / split_part2): lo = the 16-bit residual plane, hi = the bf16 working
+// copy; the same fp32 update as sgd_kernel, 4 B read + 4 B written per parameter (plus the gradient)
+__global__ __launch_bounds__(256) void sgd_split_kernel(uint16_t* lo, uint16_t* hi, const void* grad, int gdt, long n,
+                                                        float lr, float gscale) {
+  const long n4 = n / 4;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    uint2 h = *(const uint2*)(hi + 4 * i), l = *(const uint2*)(lo + 4 * i);
+    const f32x4_t g = load_grad4(grad, gdt, 4 * i);
+    float w[4];
+    split_join2(h.x, l.x, w[0], w[1]);
+    split_join2(h.y, l.y, w[2], w[3]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = __fadd_rn(w[j], __fmul_rn(-lr, __fmul_rn(gscale, g[j])));
+    split_part2(w[0], w[1], h.x, l.x);
+    split_part2(w[2], w[3], h.y, l.y);
+    *(uint2*)(hi + 4 * i) = h;
+    *(uint2*)(lo + 4 * i) = l;
+  }
+}
+
+// split master <-> fp32 (checkpoints, parameter export / import)
+__global__ __launch_bounds__(256) void split_join_kernel(const uint16_t* hi, const uint16_t* lo, float* out, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    out[i] = split_join(hi[i], lo[i]);
+}
+__global__ __launch_bounds__(256) void split_part_kernel(const float* in, uint16_t* hi, uint16_t* lo, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    split_part(in[i], hi[i], lo[i]);
+}
+
 __global__ __launch_bounds__(256) void adam_kernel(float* master, const void* grad, int gdt, float* m, float* v,
                                                    uint16_t* copy, long n, float lr, float b1, float b2, float eps,
                                                    float wd, float bc1, float bc2, float gscale) {
@@ -295,6 +325,27 @@ int dllm_sgd_step_stream(float* master, const void* grad, int grad_dtype, void* 
   return (int)hipGetLastError();
 }
 
+int dllm_sgd_split_step(void* lo, void* hi, const void* grad, int grad_dtype, long n, float lr, float gscale,
+                        void* stream) {
+  if (n % 4 || ((uintptr_t)lo | (uintptr_t)hi) % 8) return -1;
+  hipLaunchKernelGGL(sgd_split_kernel, dim3(grid_for(n / 4)), dim3(256), 0, (hipStream_t)stream, (uint16_t*)lo,
+                     (uint16_t*)hi, grad, grad_dtype, n, lr, gscale);
+  return (int)hipGetLastError();
+}
+
+// mode 0: out_f32 = join(hi, lo);  mode 1: (hi, lo) = split(in_f32)
+int dllm_split_master(void* hi, void* lo, void* f32, long n, int mode, void* stream) {
+  if (n <= 0) return 0;
+  const int g = grid_for((n + 3) / 4);
+  if (mode == 0)
+    hipLaunchKernelGGL(split_join_kernel, dim3(g), dim3(256), 0, (hipStream_t)stream, (const uint16_t*)hi,
+                       (const uint16_t*)lo, (float*)f32, n);
+  else
+    hipLaunchKernelGGL(split_part_kernel, dim3(g), dim3(256), 0, (hipStream_t)stream, (const float*)f32,
+                       (uint16_t*)hi, (uint16_t*)lo, n);
+  return (int)hipGetLastError();
+}
+
 int dllm_adam_step(float* master, const void* grad, int grad_dtype, float* m, float* v, void* copy_bf16, long n,
                    float lr, float b1, float b2, float eps, float wd, int step, float gscale, void* stream) {
   if (n % 4 || step < 1) return -1;
@@ -333,6 +384,6 @@ int dllm_occupy(int blocks, int threads, float us, float* sink, void* stream) {
   return (int)hipGetLastError();
 }
 
-int dllm_abi_version() { return 4; }
+int dllm_abi_version() { return 6; }
 
 }  // extern "C"

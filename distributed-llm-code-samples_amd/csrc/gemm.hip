@@ -16,7 +16,7 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
               const void* B, long ldb, void* C, long ldc, const void* aux, void* aux_out, long ldaux,
               int M, int N, int K, float alpha, float beta, int group_m, int force_path, void* stream,
               float lr, float b1, float b2, float eps, float wd, int step, float* opt_m, float* opt_v,
-              int ksplit, float* workspace, void* mask, int variant, int tpb, int min_bpc) {
+              int ksplit, float* workspace, void* mask, int variant, int tpb, int min_bpc, int* counters) {
   if (M <= 0 || N <= 0 || K <= 0) return -1;
   if (layout < 0 || layout > 2) return -1;
   if ((epi == EPI_GLU || epi == EPI_DGLU) && (N % 32) != 0) return -1;
@@ -34,6 +34,7 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
   a.tpb_req = tpb;
   a.min_bpc = min_bpc < 1 ? 1 : min_bpc;
   a.ws = nullptr;
+  a.cnt = nullptr;
   {
     const char* sk = getenv("DLLM_PP_SKEW");
     a.skew = sk ? atoi(sk) : 0;
@@ -42,15 +43,19 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
   const bool aligned_ptr = ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && ((uintptr_t)C % 16 == 0) &&
                            ((uintptr_t)aux % 16 == 0) && ((uintptr_t)aux_out % 16 == 0) &&
                            ((uintptr_t)opt_m % 16 == 0) && ((uintptr_t)opt_v % 16 == 0);
-  const bool opt_epi = (epi == EPI_SGD || epi == EPI_ADAM);
-  if (opt_epi && (layout != L_TN || out_dtype != DT_F32)) return -1;
+  const bool opt_epi = (epi == EPI_SGD || epi == EPI_ADAM || epi == EPI_SGDS);
+  if (opt_epi && layout != L_TN) return -1;
+  if ((epi == EPI_SGD || epi == EPI_ADAM) && out_dtype != DT_F32) return -1;
+  // split master: C = the 16-bit residual plane, aux_out = the bf16 working copy (paired 16-B rows: ld % 8 == 0)
+  if (epi == EPI_SGDS && (out_dtype != DT_BF16 || in_dtype != DT_BF16 || aux_out == nullptr)) return -1;
   if (epi == EPI_ADAM) {
     if (step < 1 || !opt_m || !opt_v) return -1;
     a.bc1 = 1.f - powf(b1, (float)step);
     a.bc2 = 1.f - powf(b2, (float)step);
   }
   int path = 2;
-  const bool aligned_lds = aligned_ptr && (lda % 8 == 0) && (ldb % 8 == 0) && (ldc % 4 == 0) && (ldaux % 4 == 0);
+  const bool aligned_lds = aligned_ptr && (lda % 8 == 0) && (ldb % 8 == 0) && (ldc % 4 == 0) && (ldaux % 4 == 0) &&
+                           (epi != EPI_SGDS || (ldc % 8 == 0 && ldaux % 8 == 0));
   if (in_dtype == DT_BF16 && M % BT_M == 0 && N % BT_N == 0 && K % BT_K == 0 && aligned_lds) path = 0;
   if (in_dtype == DT_F32 && out_dtype == DT_F32 && M % FT == 0 && N % FT == 0 && K % FK == 0 && aligned_lds) path = 1;
   if (force_path >= 0) {
@@ -66,6 +71,7 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
     if (path == 0 && (K / BT_K) % (2 * ksplit) == 0 && a.variant != 1) {
       a.ksplit = ksplit;
       a.ws = workspace;
+      a.cnt = counters;  // (M/256)*(N/256)*8 zeroed ints: combine in the kernel; null: a splitk_reduce pass
     }
   }
   if (mask != nullptr) {

@@ -78,6 +78,9 @@ struct GemmArgs {
   // gemm_bf16_pp: initial delay (x 64 clocks) of the odd workgroup slot of each CU, so the two co-resident blocks
   // start out of phase (experiment knob, DLLM_PP_SKEW; 0 = none)
   int skew;
+  // in-kernel split-K combine (SEAM instantiations): per (tile, wave) arrival counters, zero at launch and left zero
+  // by each tile's last arriver; ws then holds the per-slice partials in the accumulator-native layout
+  int* cnt;
 };
 
 // ----------------------------------------------------------------------------------------------
@@ -149,6 +152,18 @@ __device__ __forceinline__ void epi4(const GemmArgs& p, int m, int n, f32x4_t v)
     for (int r = 0; r < 4; ++r) w[r] = __fadd_rn(w[r], __fmul_rn(-p.lr, __fmul_rn(p.alpha, v[r])));
     Vec4<float>::store(p.C, ci, w);
     if (p.aux_out) Vec4<uint16_t>::store(p.aux_out, (long)m * p.ldaux + n, w);
+  } else if constexpr (EPI == EPI_SGDS) {
+    uint2* hp = (uint2*)((uint16_t*)p.aux_out + (long)m * p.ldaux + n);
+    uint2* lp = (uint2*)((uint16_t*)p.C + ci);
+    uint2 h = *hp, l = *lp;
+    float w[4];
+    split_join2(h.x, l.x, w[0], w[1]);
+    split_join2(h.y, l.y, w[2], w[3]);
+    for (int r = 0; r < 4; ++r) w[r] = __fadd_rn(w[r], __fmul_rn(-p.lr, __fmul_rn(p.alpha, v[r])));
+    split_part2(w[0], w[1], h.x, l.x);
+    split_part2(w[2], w[3], h.y, l.y);
+    *hp = h;
+    *lp = l;
   } else if constexpr (EPI == EPI_ADAM) {
     f32x4_t w = Vec4<float>::load(p.C, ci);
     f32x4_t mm = Vec4<float>::load(p.opt_m, ci);
@@ -274,7 +289,7 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
   // (the beta != 0 store path is off the FFN hot path: small batches keep the persistent kernel's
   // in-loop epilogue within the register budget)
   constexpr int COST = EPI == EPI_DACT ? WR : EPI == EPI_DGLU ? 8 * (BF ? 2 : 4) : EPI == EPI_STORE ? 4 * WR
-                     : EPI == EPI_SGD ? 8 : EPI == EPI_ADAM ? 24 : 0;
+                     : EPI == EPI_SGD || EPI == EPI_SGDS ? 8 : EPI == EPI_ADAM ? 24 : 0;
   constexpr int RB = epi_batch(COST);
   const int pc = pair_col(lane);
 #define DLLM_M(rg) (m0 + ((rg) >> 3) * 128 + wr * 64 + ((rg) & 3) * 16 + (lane & 15))
@@ -507,6 +522,40 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
 #pragma unroll
         for (int r = 0; r < RB; ++r)
           st_pair_bf16(p.aux_out, (long)DLLM_M(b0 + r) * p.ldaux + DLLM_NB(b0 + r) + pc, W[r][0], W[r][1]);
+      }
+    }
+  } else if constexpr (EPI == EPI_SGDS) {
+    // split master: hi plane = the bf16 working copy (aux_out), lo plane = the 16-bit residual (Cp), both in the
+    // paired 16-B layout: per row group one 16-B load and one 16-B store per plane (4 B read + 4 B written per
+    // parameter; the fp32 master form moves 4 B + 6 B in 5 accesses)
+#pragma unroll
+    for (int b0 = 0; b0 < 16; b0 += RB) {
+      uint4 H[RB], Lw[RB];
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        H[r] = *(const uint4*)((const uint16_t*)p.aux_out + (long)DLLM_M(b0 + r) * p.ldaux + DLLM_NB(b0 + r) + pc);
+        Lw[r] = *(const uint4*)((const uint16_t*)Cp + (long)DLLM_M(b0 + r) * p.ldc + DLLM_NB(b0 + r) + pc);
+      }
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        // after the exchange: words 0-1 hold the nt = 0 fragment's 4 columns, words 2-3 the nt = 1 fragment's
+        const uint4 h = pair_swap(uint2{H[r].x, H[r].y}, uint2{H[r].z, H[r].w});
+        const uint4 l = pair_swap(uint2{Lw[r].x, Lw[r].y}, uint2{Lw[r].z, Lw[r].w});
+        const f32x4_t g0 = DLLM_ACC(b0 + r, 0), g1 = DLLM_ACC(b0 + r, 1);
+        uint32_t hw[4] = {h.x, h.y, h.z, h.w}, lw[4] = {l.x, l.y, l.z, l.w};
+        const float gg[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float f0, f1;
+          split_join2(hw[j], lw[j], f0, f1);
+          f0 = __fadd_rn(f0, __fmul_rn(-p.lr, __fmul_rn(p.alpha, gg[2 * j])));
+          f1 = __fadd_rn(f1, __fmul_rn(-p.lr, __fmul_rn(p.alpha, gg[2 * j + 1])));
+          split_part2(f0, f1, hw[j], lw[j]);
+        }
+        *(uint4*)((uint16_t*)p.aux_out + (long)DLLM_M(b0 + r) * p.ldaux + DLLM_NB(b0 + r) + pc) =
+            pair_swap(uint2{hw[0], hw[1]}, uint2{hw[2], hw[3]});
+        *(uint4*)((uint16_t*)Cp + (long)DLLM_M(b0 + r) * p.ldc + DLLM_NB(b0 + r) + pc) =
+            pair_swap(uint2{lw[0], lw[1]}, uint2{lw[2], lw[3]});
       }
     }
   } else if constexpr (EPI == EPI_ADAM && DLLM_ADAM_PIPE) {
@@ -852,11 +901,81 @@ __device__ __forceinline__ GemmArgs reload_args() {
     __builtin_amdgcn_sched_barrier(0);                    \
   } while (0)
 
+// In-kernel split-K combine (the SEAM instantiations of gemm_bf16_8ph; replaces the separate splitk_reduce pass).
+// Every wave of every K-slice block stores its fp32 partial -- 32 x 16 B per lane, lane-interleaved, so each store
+// instruction writes 1 KB contiguous -- write-through (sc1), drains it (vmcnt(0)) and takes a ticket on its own
+// (tile, wave) counter (relaxed agent-scope atomic).  The wave that draws ksplit - 1 is the last arriver: it reads
+// all ksplit partials back with sc1 loads (they bypass this CU's L1 and the other XCDs' L2s hold none of them: no
+// acquire fence), sums them in slice order from zero -- the splitk_reduce order, so the result does not depend on
+// which slice arrives last -- resets the counter, and runs the real epilogue for its 128x64 region.  Nothing waits
+// on another block, so the protocol cannot hang, and one wave's hand-off needs no workgroup barrier (the staggered
+// wave groups of the 8-phase schedule never meet at one).  cdna_hip_programming.md §5 "Projection GEMM" item 2 and
+// §6 Guideline 16 (sc1 slab stores, relaxed agent ticket, sc1 slab loads).
+// last arriver: ac = sum of the S partials in slice order, from zero.  All S slices of a batch of CG accumulator
+// groups are loaded before any is added (S * CG * 4 <= 64 VGPRs in flight: the fragment registers are dead here), so
+// the combine costs 32 / CG memory round trips, not 32 * S.  Fully unrolled: ac is never indexed at run time.
+template <int S>
+__device__ __forceinline__ void seam_sum(f32x4_t (&ac)[2][2][4][2], __amdgpu_buffer_rsrc_t rs, int wid, int lane) {
+  constexpr int CG = 16 / S >= 8 ? 8 : 16 / S >= 4 ? 4 : 16 / S >= 2 ? 2 : 1;
+#pragma unroll
+  for (int g0 = 0; g0 < 32; g0 += CG) {
+    f32x4_t t[S][CG];
+#pragma unroll
+    for (int sl = 0; sl < S; ++sl)
+#pragma unroll
+      for (int j = 0; j < CG; ++j)
+        t[sl][j] = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
+                                                   rs, ((sl * 8 + wid) * 32 + g0 + j) * 1024 + lane * 16, 0, 16));
+#pragma unroll
+    for (int j = 0; j < CG; ++j) {
+      const int g = g0 + j;
+      f32x4_t v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int sl = 0; sl < S; ++sl) v += t[sl][j];
+      ac[g >> 4][(g >> 3) & 1][(g >> 1) & 3][g & 1] = v;
+    }
+  }
+}
+
+template <int EPI, typename OutT, int ACT>
+__device__ __forceinline__ void seam_epilogue(const GemmArgs& q, f32x4_t (&ac)[2][2][4][2], int sp, int tm0,
+                                              int tn0, int wr, int wc, int wid, int lane) {
+  typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
+  const int S = q.ksplit;
+  const int tile = (tm0 / BT_M) * (q.N / BT_N) + tn0 / BT_N;
+  // [tile][slice][wave][32 groups][64 lanes] x 16 B; one buffer resource per tile (S * 256 KiB < 2^31)
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(q.ws + (long)tile * S * 65536, (short)0, S * 65536 * 4, 0x00020000);
+  const int own = ((sp * 8 + wid) * 32) * 1024 + lane * 16;
+#pragma unroll
+  for (int g = 0; g < 32; ++g)
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, ac[g >> 4][(g >> 3) & 1][(g >> 1) & 3][g & 1]),
+                                           rs, own + g * 1024, 0, 16 /* sc1 */);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial is in memory before its ticket
+  int* c = q.cnt + tile * 8 + wid;
+  int ticket = 0;
+  if (lane == 0) ticket = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  ticket = __builtin_amdgcn_readfirstlane(ticket);
+  if (ticket != S - 1) return;
+  if (lane == 0) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: keep the loads below the ticket
+  switch (S) {
+    case 2: seam_sum<2>(ac, rs, wid, lane); break;
+    case 3: seam_sum<3>(ac, rs, wid, lane); break;
+    case 4: seam_sum<4>(ac, rs, wid, lane); break;
+    case 6: seam_sum<6>(ac, rs, wid, lane); break;
+    default: seam_sum<8>(ac, rs, wid, lane); break;  // the host splits K by 2, 3, 4, 6 or 8 only
+  }
+  epilogue_256<EPI, OutT, ACT>(q, ac, tm0, tn0, wr, wc, lane, q.C);
+}
+
 // ACT >= 0: activation of the ACT/DACT/GLU/DGLU epilogues fixed at compile time (-1: runtime p.act)
 // NPH = 8: the 8-phase schedule below (one quadrant = 16 MFMAs per wave per barrier interval).
 // NPH = 4: half-tile phases (two quadrants = 32 MFMAs per interval, two half-tiles restaged per phase):
 // halves the barrier count per MFMA (see the NPH == 4 loop).
-template <int LAYOUT, int EPI, typename OutT, bool STAGGER, int ACT = -1, int NPH = 8, bool PERS = false>
+// SEAM: split-K slices combined in the kernel (seam_epilogue); p.ksplit > 1, p.ws / p.cnt set, one slot per block.
+template <int LAYOUT, int EPI, typename OutT, bool STAGGER, int ACT = -1, int NPH = 8, bool PERS = false,
+          bool SEAM = false>
 __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
   // slot(op, hh, buf) = ((op*2 + hh)*2 + buf) * 16 KiB: A in [0, 64K), B in [64K, 128K), so every
   // fragment read is base + a 16-bit immediate
@@ -916,6 +1035,10 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
     const GemmArgs q = reload_args();
     int sp, tm0, tn0;
     tile_of(q, s, sp, tm0, tn0);
+    if constexpr (SEAM) {
+      seam_epilogue<EPI, OutT, ACT>(q, ac, sp, tm0, tn0, wr, wc, wid, lane);
+      return;
+    }
     void* out = q.C;
     if constexpr (EPI == EPI_STORE)
       if (q.ksplit > 1) out = (char*)q.C + (long)sp * q.M * q.ldc * sizeof(OutT);
@@ -1555,6 +1678,11 @@ __global__ __launch_bounds__(256) void gemm_generic(GemmArgs p) {
         const float w = __fadd_rn(W[ci], __fmul_rn(-p.lr, __fmul_rn(p.alpha, v)));
         W[ci] = w;
         if (p.aux_out) st1<uint16_t>(p.aux_out, (long)m * p.ldaux + n, w);
+      } else if constexpr (EPI == EPI_SGDS) {
+        uint16_t* hp = (uint16_t*)p.aux_out + (long)m * p.ldaux + n;
+        uint16_t* lp = (uint16_t*)p.C + (long)m * p.ldc + n;
+        const float w = __fadd_rn(split_join(*hp, *lp), __fmul_rn(-p.lr, __fmul_rn(p.alpha, v)));
+        split_part(w, *hp, *lp);
       } else if constexpr (EPI == EPI_ADAM) {
         const long ci = (long)m * p.ldc + n;
         float* W = (float*)p.C;
@@ -1718,9 +1846,21 @@ static void launch_pp(const GemmArgs& a, hipStream_t s) {
   launch_pp_act<L, E, OutT, -1>(a, s);
 }
 
-// main kernel writes partials into the workspace, then the reduction applies the epilogue
+// main kernel writes partials into the workspace, then the reduction applies the epilogue -- or, with arrival
+// counters (a.cnt) on the 8-phase family, the slices combine inside the kernel (SEAM, no second pass)
 template <int L, int E>
 static hipError_t launch_splitk(const GemmArgs& a, int out_dt, float* ws, hipStream_t s) {
+  if (a.cnt != nullptr && a.variant != 4 && a.variant != 5) {
+    GemmArgs w = a;
+    w.ws = ws;
+    w.tpb = 1;
+    const int nb = (a.M / BT_M) * (a.N / BT_N) * a.ksplit;
+    if (out_dt == DT_F32)
+      hipLaunchKernelGGL((gemm_bf16_8ph<L, E, float, true, -1, 8, false, true>), dim3(nb), dim3(512), 0, s, w);
+    else
+      hipLaunchKernelGGL((gemm_bf16_8ph<L, E, uint16_t, true, -1, 8, false, true>), dim3(nb), dim3(512), 0, s, w);
+    return hipGetLastError();
+  }
   GemmArgs w = a;
   w.C = ws;
   w.ldc = a.N;
@@ -1756,7 +1896,7 @@ constexpr bool persistent_kernel() {
   // gated (SwiGLU) stacks: the GLU forward / DGLU dgrad with a compile-time activation (round 3)
   if constexpr (L == L_NT) return bf && ((E == EPI_ACT && ACT == ACT_RELU) || E == EPI_STORE || (E == EPI_GLU && ACT >= 0));
   if constexpr (L == L_NN) return bf && ((E == EPI_DACT && ACT == ACT_RELU) || E == EPI_STORE || (E == EPI_DGLU && ACT >= 0));
-  return E == EPI_STORE || E == EPI_SGD;
+  return E == EPI_STORE || E == EPI_SGD || E == EPI_SGDS;
 }
 
 template <int L, int E, typename OutT, int ACT, int NPH>
@@ -1873,10 +2013,15 @@ static hipError_t dispatch_opt(int path, const GemmArgs& a, int in_dt, hipStream
       hipLaunchKernelGGL((gemm_bf16_256<L_TN, E, float>), dim3(nb), dim3(512), 0, s, a);
     return hipGetLastError();
   }
-  if (path == 1) return launch_f32<L_TN, E>(a, s);
   dim3 grid((a.N + 63) / 64, (a.M + 63) / 64);
-  if (in_dt == DT_BF16) hipLaunchKernelGGL((gemm_generic<L_TN, E, uint16_t, float>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((gemm_generic<L_TN, E, float, float>), grid, dim3(256), 0, s, a);
+  if constexpr (E == EPI_SGDS) {  // split masters exist only next to a bf16 working copy: bf16 inputs
+    if (path == 1 || in_dt != DT_BF16) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((gemm_generic<L_TN, E, uint16_t, float>), grid, dim3(256), 0, s, a);
+  } else {
+    if (path == 1) return launch_f32<L_TN, E>(a, s);
+    if (in_dt == DT_BF16) hipLaunchKernelGGL((gemm_generic<L_TN, E, uint16_t, float>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((gemm_generic<L_TN, E, float, float>), grid, dim3(256), 0, s, a);
+  }
   return hipGetLastError();
 }
 

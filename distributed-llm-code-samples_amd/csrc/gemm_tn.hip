@@ -9,7 +9,9 @@ hipError_t dispatch_tn(int path, int epi, const GemmArgs& a, int in_dt, int out_
 }
 
 hipError_t dispatch_tn_opt(int path, int epi, const GemmArgs& a, int in_dt, hipStream_t s) {
-  return epi == EPI_SGD ? dispatch_opt<EPI_SGD>(path, a, in_dt, s) : dispatch_opt<EPI_ADAM>(path, a, in_dt, s);
+  if (epi == EPI_SGD) return dispatch_opt<EPI_SGD>(path, a, in_dt, s);
+  if (epi == EPI_SGDS) return dispatch_opt<EPI_SGDS>(path, a, in_dt, s);
+  return dispatch_opt<EPI_ADAM>(path, a, in_dt, s);
 }
 
 }  // namespace dllm

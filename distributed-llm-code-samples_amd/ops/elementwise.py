@@ -119,6 +119,30 @@ def sgd_step_(master: torch.Tensor, grad: torch.Tensor, lr: float, copy: torch.T
         copy.copy_(master)
 
 
+def sgd_split_step_(lo: torch.Tensor, hi: torch.Tensor, grad: torch.Tensor, lr: float,
+                    grad_scale: float = 1.0) -> None:
+    """``sgd_step_`` on a split master (``ops/master.py``): ``lo`` the int16 residual plane, ``hi`` the bf16
+    working copy; the fp32 master they encode is updated exactly as ``sgd_step_`` updates an fp32 master."""
+    if lo.dtype != torch.int16 or hi.dtype != torch.bfloat16 or lo.numel() != hi.numel():
+        raise TypeError("sgd_split_step_ takes an int16 residual plane and its bf16 working copy")
+    if lo.device.type == "cuda":
+        n = lo.numel()
+        if n % 4 or not (lo.is_contiguous() and hi.is_contiguous() and grad.is_contiguous()):
+            raise ValueError("sgd_split_step_ on GPU needs contiguous buffers with numel % 4 == 0")
+        rc = _native.lib().dllm_sgd_split_step(lo.data_ptr(), hi.data_ptr(), grad.data_ptr(), _grad_code(grad), n,
+                                               float(lr), float(grad_scale), _native.stream_ptr(lo.device))
+        _native.check(rc, "dllm_sgd_split_step")
+        return
+    from .master import join_master, set_master_
+
+    w = join_master(hi, lo)
+    g = grad.float()
+    if grad_scale != 1.0:
+        g = g * grad_scale
+    w.add_(-lr * g)
+    set_master_(hi, lo, w)
+
+
 def adam_step_(master: torch.Tensor, grad: torch.Tensor, m: torch.Tensor, v: torch.Tensor, step: int, lr: float,
                b1: float = 0.9, b2: float = 0.95, eps: float = 1e-8, wd: float = 0.0,
                copy: torch.Tensor | None = None, grad_scale: float = 1.0) -> None:

@@ -18,6 +18,8 @@ followed by an epilogue:
 * ``"sgd"``:   weight-gradient GEMM fused with the optimizer: ``C`` is the fp32 master weight, updated in place
   ``C += -lr·alpha·acc`` (reference ``param.add_(-LR*grad)``), ``aux_out`` = its bf16 working copy
 * ``"adam"``:  same with fused AdamW; ``opt_m``/``opt_v`` share ``C``'s layout
+* ``"sgd_split"``: ``"sgd"`` on a split master (``ops/master.py``): ``C`` is the int16 residual plane, ``aux_out``
+  (required) the bf16 working copy; together they hold the fp32 master, updated exactly as ``"sgd"`` updates it
 
 CUDA (HIP) tensors run the hand-written gfx950 kernels of ``csrc/gemm_kernels.h``; CPU tensors run the torch
 reference below (used by the CPU/gloo tests and as the numerics oracle).  There is no silent fallback:
@@ -30,9 +32,10 @@ import torch
 from .. import _native
 from ..utils import observe as _observe
 from .activations import act_code, act_fwd, act_grad
+from .master import join_master, set_master_
 
 LAYOUTS = {"nt": 0, "nn": 1, "tn": 2}
-EPIS = {"store": 0, "act": 1, "dact": 2, "glu": 3, "dglu": 4, "sgd": 5, "adam": 6}
+EPIS = {"store": 0, "act": 1, "dact": 2, "glu": 3, "dglu": 4, "sgd": 5, "adam": 6, "sgd_split": 7}
 FORCE = {None: -1, "mfma_bf16": 0, "mfma_f32": 1, "generic": 2, "bf16x6": -1}
 
 
@@ -109,6 +112,10 @@ def _torch_gemm(a, b, layout, out, epi, act, aux, aux_out, alpha, beta, opt=None
         out.add_(-opt["lr"] * (alpha * acc).to(out.dtype))
         if aux_out is not None:
             aux_out.copy_(out)
+    elif epi == "sgd_split":
+        w = join_master(aux_out, out)
+        w.add_(-opt["lr"] * (alpha * acc).to(torch.float32))
+        set_master_(aux_out, out, w)
     elif epi == "adam":
         g = (alpha * acc).to(out.dtype)
         b1, b2, step = opt["b1"], opt["b2"], opt["step"]
@@ -229,6 +236,29 @@ def _splitk_workspace(numel: int, device: torch.device) -> torch.Tensor:
     return ws
 
 
+# In-kernel split-K combine (csrc/gemm_kernels.h seam_epilogue): per (tile, wave) arrival counters, zeroed once here;
+# every launch leaves them zero again (each tile's last arriver resets its counter), so no per-call memset.  Cached per
+# (device, stream) like the partial workspace.  _SEAM["enabled"] False: the separate splitk_reduce pass instead.
+_CNT: dict = {}
+_SEAM = {"enabled": True}
+
+
+def _splitk_counters(n: int, device: torch.device) -> torch.Tensor:
+    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
+    c = _CNT.get(key)
+    if c is None or c.numel() < n:
+        c = torch.zeros(n, dtype=torch.int32, device=device)
+        _CNT[key] = c
+    return c
+
+
+def set_splitk_seam(enabled: bool) -> bool:
+    """Combine split-K slices inside the GEMM kernel (default) or in a separate reduction pass; returns the old value."""
+    old = _SEAM["enabled"]
+    _SEAM["enabled"] = bool(enabled)
+    return old
+
+
 def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None = None, *, epi: str = "store",
          act: str = "none", aux: torch.Tensor | None = None, aux_out: torch.Tensor | None = None,
          alpha: float = 1.0, beta: float = 0.0, out_dtype: torch.dtype | None = None, group_m: int = 4,
@@ -258,6 +288,11 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
         for t in (opt_m, opt_v):
             if t is not None and (t.shape != out.shape or t.stride() != out.stride()):
                 raise ValueError("optimizer moments must share the master weight's layout")
+    if epi == "sgd_split":
+        if layout != "tn" or out.dtype != torch.int16 or aux_out is None or aux_out.dtype != torch.bfloat16 \
+                or aux_out.shape != out.shape or a.dtype != torch.bfloat16:
+            raise ValueError("sgd_split needs the TN layout, bf16 operands, an int16 residual plane as out and its "
+                             "bf16 working copy as aux_out")
     if a.device.type != "cuda":
         opt = {"lr": lr, "b1": betas[0], "b2": betas[1], "eps": eps, "wd": wd, "step": step, "m": opt_m, "v": opt_v}
         return _torch_gemm(a, b, layout, out, epi, act, aux, aux_out, alpha, beta, opt)
@@ -275,18 +310,21 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
     auxt = aux if aux is not None else aux_out
     if auxt is not None:
         _check_rowmajor(auxt, "aux")
-        if epi in ("sgd", "adam"):
+        if epi in ("sgd", "adam", "sgd_split"):
             if auxt.dtype != torch.bfloat16 or auxt.shape != out.shape:
                 raise TypeError("fused-optimizer aux_out must be the bf16 copy of the master weight")
         elif auxt.dtype != out.dtype:
             raise TypeError("aux / aux_out must have the output dtype")
     L = _native.lib()
-    in_dt, out_dt = _native.dtype_code(a.dtype), _native.dtype_code(out.dtype)
-    ksplit, ws = 1, None
+    in_dt = _native.dtype_code(a.dtype)
+    out_dt = _native.dtype_code(torch.bfloat16 if out.dtype == torch.int16 else out.dtype)  # 16-bit planes
+    ksplit, ws, cnt = 1, None, None
     if a.dtype == torch.bfloat16 and force in (None, "mfma_bf16"):
         ksplit = choose_ksplit(M, N, K)
         if ksplit > 1 and L.dllm_gemm_path(in_dt, out_dt, M, N, K, a.stride(0), b.stride(0), out.stride(0)) == 0:
             ws = _splitk_workspace(ksplit * M * N, a.device)
+            if _SEAM["enabled"]:
+                cnt = _splitk_counters((M // 256) * (N // 256) * 8, a.device)
         else:
             ksplit = 1
     obs = _observe.active()
@@ -303,7 +341,8 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
                      opt_v.data_ptr() if opt_v is not None else None, ksplit,
                      ws.data_ptr() if ws is not None else None,
                      _mask_ptr(mask, M, N) if mask is not None else None,
-                     BF16_VARIANTS[_VARIANT["name"]], _POLICY["tpb"], _POLICY["min_bpc"])
+                     BF16_VARIANTS[_VARIANT["name"]], _POLICY["tpb"], _POLICY["min_bpc"],
+                     cnt.data_ptr() if cnt is not None else None)
     _native.check(rc, f"dllm_gemm({layout},{epi},M={M},N={N},K={K})")
     if obs is not None:
         obs.gemm_end()

@@ -43,7 +43,8 @@ import torch
 
 from ..models.ffn import (deinterleave_w13, interleave_w13, layer_bwd, layer_fwd, needs_preact,
                           recompute_fwd1)
-from ..ops.elementwise import adam_step_, cast_, sgd_step_
+from ..ops.elementwise import adam_step_, cast_, sgd_split_step_, sgd_step_
+from ..ops.master import join_flat, part_flat, split_master
 from ..utils.config import TrainConfig
 from . import comm
 from .mesh import Mesh
@@ -215,23 +216,33 @@ class FFNTrainer:
                 goff += n
             self.shard_total = goff
         # ---- flat state ----------------------------------------------------------------------------
-        self.master = torch.zeros(self.shard_total if self.zero else self.total, dtype=torch.float32, device=dev)
-        self.shared_copy = self.cd == torch.float32 and not self.zero
-        self.copy = self.master if self.shared_copy else torch.zeros(self.total, dtype=self.cd, device=dev)
         # no gradient collective (single device / pure TP): the optimizer runs inside the wgrad GEMMs and
         # no flat gradient buffer exists at all
         no_coll = not (self.ddp or self.fsdp or self.zero)
         # side-stream optimizer: wgrad GEMMs store the gradient, a low-occupancy SGD kernel on its own
         # stream updates the weight while the next GEMMs run; the forward waits per weight
         self.side_opt = (no_coll and cfg.side_optimizer > 0 and cfg.optimizer == "sgd" and dev.type == "cuda")
+        # Split master (bf16 SGD): the fp32 master is the bf16 working copy (hi) plus an int16 residual plane (lo),
+        # bitwise the same fp32 values (ops/master.py).  4 B/param of weight state instead of 6 B, and every update
+        # (fused wgrad epilogue or flat kernel) reads 4 B and writes 4 B per parameter instead of 4 B + 6 B.
+        nmaster = self.shard_total if self.zero else self.total
+        self.split = (cfg.master == "split" and self.cd == torch.bfloat16 and cfg.optimizer == "sgd"
+                      and not self.side_opt)
+        if cfg.master not in ("split", "fp32"):
+            raise ValueError(f"unknown master format {cfg.master!r}")
+        self._master = None if self.split else torch.zeros(nmaster, dtype=torch.float32, device=dev)
+        self.master_lo = torch.zeros(nmaster, dtype=torch.int16, device=dev) if self.split else None
+        self._master_stage = None  # split: the fp32 master last materialised by `master` (written back by refresh_copy)
+        self.shared_copy = self.cd == torch.float32 and not self.zero
+        self.copy = self._master if self.shared_copy else torch.zeros(self.total, dtype=self.cd, device=dev)
         self.fused_opt = cfg.fused_optimizer and no_coll and not self.side_opt
         self.grads = torch.zeros(0 if self.fused_opt else self.total, dtype=self.gd, device=dev)
         if self.side_opt:
             self.opt_stream_side = torch.cuda.Stream(device=dev)
             self.opt_done = {}
         if cfg.optimizer == "adam":
-            self.adam_m = torch.zeros(self.master.numel(), dtype=torch.float32, device=dev)
-            self.adam_v = torch.zeros(self.master.numel(), dtype=torch.float32, device=dev)
+            self.adam_m = torch.zeros(nmaster, dtype=torch.float32, device=dev)
+            self.adam_v = torch.zeros(nmaster, dtype=torch.float32, device=dev)
 
         # ---- FSDP rings --------------------------------------------------------------------------
         if self.fsdp:
@@ -345,10 +356,59 @@ class FFNTrainer:
     def _view(self, flat: torch.Tensor, e: Entry) -> torch.Tensor:
         return flat[e.offset:e.offset + e.numel].view(e.shape)
 
+    @property
+    def master(self) -> torch.Tensor:
+        """The fp32 master state this rank stores (full layout, FSDP row shards, or the ZeRO owned-shard layout).
+
+        fp32 format: the live buffer.  Split format: a materialised fp32 copy (joined from the bf16 working copy and
+        the int16 residual plane); writes to it take effect when ``refresh_copy`` runs (checkpoint load)."""
+        if not self.split:
+            return self._master
+        self._master_stage = self._join_master()
+        return self._master_stage
+
+    @property
+    def master_bytes(self) -> int:
+        """Bytes of master-weight state besides the working copy: the fp32 master, or the split format's residual
+        plane."""
+        t = self.master_lo if self.split else self._master
+        return t.numel() * t.element_size()
+
+    def _hi_shard(self) -> list:
+        """Split format: the working-copy ranges that hold this rank's master state, as (copy_lo, copy_hi, state_off)."""
+        if self.zero:
+            return [(ss, se, go) for ss, se, go in self.bucket_shard]
+        return [(0, self.total, 0)]
+
+    def master_slice(self, a: int, b: int) -> torch.Tensor:
+        """fp32 master state [a, b) of this rank's master layout (split: joined for that range only)."""
+        if not self.split:
+            return self._master[a:b]
+        out = torch.empty(b - a, dtype=torch.float32, device=self.device)
+        for ca, cb, go in self._hi_shard():
+            lo_, hi_ = max(a, go), min(b, go + (cb - ca))
+            if lo_ < hi_:
+                join_flat(self.copy[ca + lo_ - go:ca + hi_ - go], self.master_lo[lo_:hi_], out[lo_ - a:hi_ - a])
+        return out
+
+    def _join_master(self) -> torch.Tensor:
+        out = torch.empty(self.master_lo.numel(), dtype=torch.float32, device=self.device)
+        for a, b, go in self._hi_shard():
+            join_flat(self.copy[a:b], self.master_lo[go:go + (b - a)], out[go:go + (b - a)])
+        return out
+
+    def _store_master(self, w: torch.Tensor) -> None:
+        """Split format: set the master state from an fp32 buffer of the master layout (hi into the working copy's
+        owned ranges, lo into the residual plane)."""
+        for a, b, go in self._hi_shard():
+            part_flat(w[go:go + (b - a)], self.copy[a:b], self.master_lo[go:go + (b - a)])
+
     def master_view(self, l: int, name: str) -> torch.Tensor:
         if self.zero:
             raise RuntimeError("ZeRO keeps only this rank's shard of the fp32 master (see full_flat)")
-        return self._view(self.master, self.entry[(l, name)])
+        if self.split:
+            raise RuntimeError("split master: the fp32 master is copy_view + the residual plane (master_lo)")
+        return self._view(self._master, self.entry[(l, name)])
 
     def _owned_segments(self, lo: int, hi: int):
         """ZeRO: the parts of flat range [lo, hi) this rank owns, as (flat_lo, flat_hi, shard_offset)."""
@@ -460,7 +520,8 @@ class FFNTrainer:
         rank; CPU or device)."""
         if len(layers) != self.L:
             raise ValueError("layer count mismatch")
-        target = self.master if flat is None else flat
+        is_master = flat is None
+        target = (None if self.split else self._master) if is_master else flat
         d, dr = self.mesh.dp, self.mesh.dp_rank
         for l, p in enumerate(layers):
             loc = self._local_from_full(p)
@@ -468,19 +529,31 @@ class FFNTrainer:
                 src = loc[name]
                 e = self.entry[(l, name)]
                 if self.zero:
-                    srcf = src.to(device=target.device, dtype=torch.float32).reshape(-1)
+                    srcf = src.to(device=self.device, dtype=torch.float32).reshape(-1)
+                    if is_master and self.split:
+                        # every rank writes the whole working copy (hi) in the owner's rounding, the owned lo pieces
+                        hi = self.copy[e.offset:e.offset + e.numel]
+                        lo = torch.empty(e.numel, dtype=torch.int16, device=self.device)
+                        part_flat(srcf, hi, lo)
+                        for a, b, go in self._owned_segments(e.offset, e.offset + e.numel):
+                            self.master_lo[go:go + (b - a)].copy_(lo[a - e.offset:b - e.offset])
+                        continue
                     for a, b, go in self._owned_segments(e.offset, e.offset + e.numel):
                         target[go:go + (b - a)].copy_(srcf[a - e.offset:b - e.offset])
-                    if target is self.master:
+                    if is_master:
                         self._view(self.copy, e).copy_(srcf.view(e.shape))  # RNE cast, as cast_
                     continue
                 if self.fsdp:
                     rows = src.shape[0] // d
                     src = src[dr * rows:(dr + 1) * rows]
+                if is_master and self.split:   # per weight: no full-size fp32 transient
+                    part_flat(src.to(device=self.device, dtype=torch.float32).reshape(-1),
+                              self.copy[e.offset:e.offset + e.numel], self.master_lo[e.offset:e.offset + e.numel])
+                    continue
                 self._view(target, e).copy_(src.to(torch.float32))
-        if target is self.master and not self.shared_copy and not self.zero:
-            cast_(self.master, self.copy)
-        if self.fsdp and target is self.master:
+        if is_master and not self.split and not self.shared_copy and not self.zero:
+            cast_(self._master, self.copy)
+        if self.fsdp and is_master:
             self.fsdp_sync()
             self.ag_next.clear()  # gathered rings hold the old weights
 
@@ -491,15 +564,23 @@ class FFNTrainer:
         if self.fsdp:
             self.fsdp_sync()
             self.ag_next.clear()  # gathered rings hold the old weights
-        if self.shared_copy:
+        if self.split:
+            # the fp32 master was written through the buffer `master` last materialised (flat_buffers)
+            if self._master_stage is not None:
+                self._store_master(self._master_stage)
+                self._master_stage = None
+        elif self.shared_copy:
+            return
+        elif not self.zero:
+            cast_(self._master, self.copy)
             return
         if not self.zero:
-            cast_(self.master, self.copy)
             return
         grp = self.mesh.group("dp_ag")
         for b, (s_, e_, _) in enumerate(self.buckets):
             ss, se, go = self.bucket_shard[b]
-            self.copy[ss:se].copy_(self.master[go:go + (se - ss)])
+            if not self.split:
+                self.copy[ss:se].copy_(self._master[go:go + (se - ss)])
             src = self.copy[ss:se].clone() if self.device.type != "cuda" else self.copy[ss:se]
             comm.all_gather_into(self.copy[s_:e_], src, grp, async_op=False)
 
@@ -557,6 +638,9 @@ class FFNTrainer:
     # ------------------------------------------------------------------------------------------------
     def _fused_wgrad_kw(self, l: int, name: str) -> dict:
         cfg = self.cfg
+        if self.split:
+            return {"out": self._view(self.master_lo, self.entry[(l, name)]), "epi": "sgd_split", "lr": cfg.lr,
+                    "aux_out": self.copy_view(l, name)}
         kw = {"out": self.master_view(l, name), "epi": cfg.optimizer, "lr": cfg.lr}
         if not self.shared_copy:
             kw["aux_out"] = self.copy_view(l, name)
@@ -568,7 +652,10 @@ class FFNTrainer:
 
     def _opt(self, s: int, e: int) -> None:
         cfg = self.cfg
-        master, grad = self.master[s:e], self.grads[s:e]
+        if self.split:  # full or FSDP-shard layout: the residual plane shares the working copy's offsets
+            sgd_split_step_(self.master_lo[s:e], self.copy[s:e], self.grads[s:e], cfg.lr)
+            return
+        master, grad = self._master[s:e], self.grads[s:e]
         copy = None if self.shared_copy else self.copy[s:e]
         if cfg.optimizer == "sgd":
             sgd_step_(master, grad, cfg.lr, copy=copy)
@@ -587,7 +674,7 @@ class FFNTrainer:
             st.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(st):
                 copy = None if self.shared_copy else self.copy[s_:e_]
-                sgd_step_(self.master[s_:e_], self.grads[s_:e_], self.cfg.lr, copy=copy,
+                sgd_step_(self._master[s_:e_], self.grads[s_:e_], self.cfg.lr, copy=copy,
                           max_blocks=self.cfg.side_optimizer)
                 ev = torch.cuda.Event()
                 ev.record(st)
@@ -635,10 +722,12 @@ class FFNTrainer:
         n = se - ss
         cfg = self.cfg
         g = self.gshard[go:go + n]
-        master = self.master[go:go + n]
         bf16_copy = self.cd == torch.bfloat16
         copy = self.copy[ss:se] if bf16_copy else None  # bf16: written by the optimizer kernel itself
-        if cfg.optimizer == "sgd":
+        master = None if self.split else self._master[go:go + n]
+        if self.split:
+            sgd_split_step_(self.master_lo[go:go + n], copy, g, cfg.lr)
+        elif cfg.optimizer == "sgd":
             sgd_step_(master, g, cfg.lr, copy=copy)
         else:
             adam_step_(master, g, self.adam_m[go:go + n], self.adam_v[go:go + n], self.step_count, cfg.lr,

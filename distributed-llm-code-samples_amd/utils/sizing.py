@@ -25,10 +25,12 @@ def _round_up(n: int, a: int) -> int:
 def plan(D: int, F: int, L: int, tokens: int, dp: int = 1, tp: int = 1, mode: str = "none", gated: bool = False,
          act: str = "relu", dtype: str = "bf16", grad_dtype: str = "bf16", optimizer: str = "sgd",
          recompute: str = "none", relu_mask: bool = True, sequence_parallel: bool = False,
-         align: int = 64, wgrad_stream: bool = False) -> dict:
+         align: int = 64, wgrad_stream: bool = False, master: str = "split") -> dict:
     """Per-rank bytes by buffer (and GiB totals).  ``mode``: none | ddp | zero | fsdp (over ``dp`` ranks).
     ``wgrad_stream``: the concurrent weight-gradient stream (single device, fused optimizer, kept activations, no
-    TP) rotates two dgrad and three dx buffers instead of one and two (``FFNTrainer.da_ring`` / ``dxb``)."""
+    TP) rotates two dgrad and three dx buffers instead of one and two (``FFNTrainer.da_ring`` / ``dxb``).
+    ``master``: "split" keeps a bf16 SGD run's fp32 master as the working copy plus an int16 residual plane
+    (``master_residual``, 2 B/param) instead of a separate fp32 buffer (``master_fp32``, 4 B/param)."""
     cd = 2 if dtype == "bf16" else 4
     gd = 2 if grad_dtype == "bf16" else 4
     multi = dp > 1
@@ -40,7 +42,10 @@ def plan(D: int, F: int, L: int, tokens: int, dp: int = 1, tp: int = 1, mode: st
     total = L * (_round_up(own(R1 * D), al) + _round_up(own(D * F_loc), al))
     master_n = total // dp if zero else total
     b = {}
-    b["master_fp32"] = master_n * 4
+    if master == "split" and dtype == "bf16" and optimizer == "sgd":
+        b["master_residual"] = master_n * 2
+    else:
+        b["master_fp32"] = master_n * 4
     shared_copy = cd == 4 and not zero
     b["compute_copy"] = 0 if shared_copy else total * cd
     fused = not (ddp or zero or fsdp)
@@ -70,7 +75,7 @@ def plan(D: int, F: int, L: int, tokens: int, dp: int = 1, tp: int = 1, mode: st
     b["dx_buffers"] = (3 if ws else 2) * T * D * cd
     if sp:
         b["sp_buffers"] = (3 + (L if keep else 0)) * T * D * cd + 2 * Tl * D * cd
-    state = sum(v for k, v in b.items() if k in ("master_fp32", "compute_copy", "grads", "adam_moments",
+    state = sum(v for k, v in b.items() if k in ("master_fp32", "master_residual", "compute_copy", "grads", "adam_moments",
                                                    "zero_grad_shard", "fsdp_weight_ring", "fsdp_grad_ring"))
     tot = sum(b.values())
     g = 2**30

@@ -1,0 +1,101 @@
+"""Split fp32 master (bf16 working copy + int16 residual, ops/master.py) on the GPU kernels.
+
+Every form of the SGD update -- the fused weight-gradient epilogue of each bf16 kernel family (256x256 2-stage,
+8-phase one tile per block and persistent, 256x128 two-per-CU, split-K reduction, generic odd shapes) and the flat
+optimizer kernel -- must leave bitwise the fp32 master the fp32-master form leaves, with the working copy equal to
+that master rounded half away from zero.  The engine check: one training step from bf16-representable weights (no
+rounding ties at the start) gives bitwise the fp32-master engine's master.
+"""
+import pytest
+import torch
+
+from dllm.ops.gemm import gemm, set_bf16_variant, set_splitk, set_tiles_per_block
+from dllm.ops.master import join_flat, join_master, part_flat, split_master
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair(M, N, K, seed):
+    g = torch.Generator().manual_seed(seed)
+    a = torch.randn(K, M, generator=g).to(torch.bfloat16).cuda()
+    b = torch.randn(K, N, generator=g).to(torch.bfloat16).cuda()
+    w = (torch.randn(M, N, generator=g) * 0.02).cuda()
+    return a, b, w
+
+
+def _check_same_update(a, b, w, lr=1e-2):
+    m32, c16 = w.clone(), w.to(torch.bfloat16)
+    gemm(a, b, "tn", out=m32, epi="sgd", lr=lr, aux_out=c16)
+    hi, lo = split_master(w)
+    gemm(a, b, "tn", out=lo, epi="sgd_split", lr=lr, aux_out=hi)
+    torch.cuda.synchronize()
+    assert torch.equal(join_master(hi, lo).view(torch.int32), m32.view(torch.int32))
+    assert torch.equal(hi.view(torch.int16), split_master(m32)[0].view(torch.int16))
+
+
+@pytest.mark.parametrize("variant,tpb", [("2stage", 1), ("8phase_stagger", 1), ("8phase_stagger", 8), ("pp", 1),
+                                         ("pp", 8)])
+def test_fused_sgd_split_equals_fp32_master(variant, tpb):
+    old_v, old_t = set_bf16_variant(variant), set_tiles_per_block(tpb)
+    try:
+        a, b, w = _pair(2048, 1536, 1024, 5)   # 48 tiles: persistent grids hold several per block
+        _check_same_update(a, b, w)
+    finally:
+        set_bf16_variant(old_v)
+        set_tiles_per_block(old_t)
+
+
+def test_fused_sgd_split_splitk_and_generic():
+    set_splitk(True)
+    a, b, w = _pair(512, 512, 2048, 6)         # 4 tiles -> split-K reduction applies the update
+    _check_same_update(a, b, w)
+    a, b, w = _pair(200, 136, 96, 7)           # odd shape -> generic kernel
+    _check_same_update(a, b, w)
+
+
+def test_flat_sgd_split_and_join_kernels():
+    from dllm.ops.elementwise import sgd_split_step_, sgd_step_
+
+    g = torch.Generator().manual_seed(8)
+    n = 1 << 20
+    w = (torch.randn(n, generator=g) * 0.02).cuda()
+    grad = torch.randn(n, generator=g).to(torch.bfloat16).cuda()
+    m32, c16 = w.clone(), w.to(torch.bfloat16)
+    sgd_step_(m32, grad, 0.1, copy=c16)
+    hi = torch.empty(n, dtype=torch.bfloat16, device="cuda")
+    lo = torch.empty(n, dtype=torch.int16, device="cuda")
+    part_flat(w, hi, lo)
+    h_ref, l_ref = split_master(w)
+    assert torch.equal(hi.view(torch.int16), h_ref.view(torch.int16)) and torch.equal(lo, l_ref)
+    sgd_split_step_(lo, hi, grad, 0.1)
+    assert torch.equal(join_flat(hi, lo).view(torch.int32), m32.view(torch.int32))
+    # every 32-bit pattern survives the native split / join
+    u = torch.randint(-2**31, 2**31 - 1, (n,), generator=g, dtype=torch.int32).cuda()
+    part_flat(u.view(torch.float32), hi, lo)
+    assert torch.equal(join_flat(hi, lo).view(torch.int32), u)
+
+
+@pytest.mark.parametrize("wgrad_stream", [False, True])
+def test_engine_split_master_step_equals_fp32(wgrad_stream):
+    from dllm.parallel.engine import FFNTrainer
+    from dllm.parallel.mesh import Mesh
+    from dllm.utils.config import ModelConfig, TrainConfig
+    from dllm.utils.data import DeviceMockData
+
+    D, F, L = 512, 2048, 3
+    g = torch.Generator().manual_seed(9)
+    # bf16-representable weights: both formats start from the same working copy (no rounding ties)
+    layers = [{"w1": (torch.randn(F, D, generator=g) * 0.02).bfloat16().float(),
+               "w2": (torch.randn(D, F, generator=g) * 0.02).bfloat16().float()} for _ in range(L)]
+    outs = []
+    for fmt in ("fp32", "split"):
+        cfg = TrainConfig(model=ModelConfig(D, F, L), batch_size=2, seq_len=512, dtype="bf16", grad_dtype="bf16",
+                          lr=1e-2, master=fmt, wgrad_stream=wgrad_stream)
+        eng = FFNTrainer(cfg, Mesh(), torch.device("cuda"))
+        assert eng.split == (fmt == "split")
+        eng.load_full_params(layers)
+        x, dy = DeviceMockData(cfg.tokens, D, torch.bfloat16, torch.device("cuda")).fill(3)
+        eng.train_step(x, dy)
+        torch.cuda.synchronize()
+        outs.append(eng.master.clone())
+    assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
