@@ -384,6 +384,6 @@ int dllm_occupy(int blocks, int threads, float us, float* sink, void* stream) {
   return (int)hipGetLastError();
 }
 
-int dllm_abi_version() { return 6; }
+int dllm_abi_version() { return 7; }
 
 }  // extern "C"

@@ -16,7 +16,8 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
               const void* B, long ldb, void* C, long ldc, const void* aux, void* aux_out, long ldaux,
               int M, int N, int K, float alpha, float beta, int group_m, int force_path, void* stream,
               float lr, float b1, float b2, float eps, float wd, int step, float* opt_m, float* opt_v,
-              int ksplit, float* workspace, void* mask, int variant, int tpb, int min_bpc, int* counters) {
+              int ksplit, float* workspace, void* mask, int variant, int tpb, int min_bpc, int* counters,
+              long ws_numel) {
   if (M <= 0 || N <= 0 || K <= 0) return -1;
   if (layout < 0 || layout > 2) return -1;
   if ((epi == EPI_GLU || epi == EPI_DGLU) && (N % 32) != 0) return -1;
@@ -35,6 +36,7 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
   a.min_bpc = min_bpc < 1 ? 1 : min_bpc;
   a.ws = nullptr;
   a.cnt = nullptr;
+  a.ws_numel = 0;
   {
     const char* sk = getenv("DLLM_PP_SKEW");
     a.skew = sk ? atoi(sk) : 0;
@@ -64,6 +66,11 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
     path = force_path;
   }
   if (path == 2 && epi == EPI_GLU && aux_out == nullptr) return -1;
+  if (epi == EPI_SGDS && ksplit <= 1 && workspace != nullptr && ws_numel > 0) {
+    // deferred fused update (persistent 8-phase grids): the workspace holds one 256 KiB slab per block
+    a.ws = workspace;
+    a.ws_numel = ws_numel;
+  }
   if (ksplit > 1) {
     // split-K only on the bf16 8-phase path (each slice an even number of 64-deep K-tiles); a request
     // that cannot be honoured (other kernel family / forced 2-stage variant) runs unsplit

@@ -81,6 +81,7 @@ struct GemmArgs {
   // in-kernel split-K combine (SEAM instantiations): per (tile, wave) arrival counters, zero at launch and left zero
   // by each tile's last arriver; ws then holds the per-slice partials in the accumulator-native layout
   int* cnt;
+  long ws_numel;  // floats available at ws (DEFER slabs: 65536 per block)
 };
 
 // ----------------------------------------------------------------------------------------------
@@ -974,12 +975,13 @@ __device__ __forceinline__ void seam_epilogue(const GemmArgs& q, f32x4_t (&ac)[2
 // NPH = 4: half-tile phases (two quadrants = 32 MFMAs per interval, two half-tiles restaged per phase):
 // halves the barrier count per MFMA (see the NPH == 4 loop).
 // SEAM: split-K slices combined in the kernel (seam_epilogue); p.ksplit > 1, p.ws / p.cnt set, one slot per block.
+// DEFER (persistent EPI_SGDS only): a tile's optimizer update runs under the NEXT tile's main loop (see below).
 template <int LAYOUT, int EPI, typename OutT, bool STAGGER, int ACT = -1, int NPH = 8, bool PERS = false,
-          bool SEAM = false>
+          bool SEAM = false, bool DEFER = false>
 __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
   // slot(op, hh, buf) = ((op*2 + hh)*2 + buf) * 16 KiB: A in [0, 64K), B in [64K, 128K), so every
-  // fragment read is base + a 16-bit immediate
-  __shared__ __attribute__((aligned(16))) char smem[8 * HT];
+  // fragment read is base + a 16-bit immediate.  DEFER adds a 32 KiB side region at 128K (4 KiB per wave).
+  __shared__ __attribute__((aligned(16))) char smem[8 * HT + (DEFER ? 32768 : 0)];
   DLLM_LDS char* lds = (DLLM_LDS char*)smem;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1056,6 +1058,70 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
     const uint32_t* off = op == 0 ? aoff : boff;
     glds16((const uint16_t*)((const char*)src + off[0]), dst + wid * 1024);
     glds16((const uint16_t*)((const char*)src + off[1]), dst + (wid + 8) * 1024);
+  };
+
+  // ---- DEFER: the fused split-master SGD update of a tile, spread over the next tile's main loop ----
+  // A persistent block that has another tile to run does not update the master at the end of a tile: each thread
+  // stores its 128 fp32 accumulators to the block's scratch slab (p.ws, 256 KiB per block, lane-interleaved so every
+  // store instruction writes 1 KiB) and moves on.  During the next tile's iterations 0..15 every wave LDS-DMAs one
+  // row group's worth -- its two accumulator groups from the slab, the paired hi / lo words of the master -- into its
+  // own 4 KiB of a side LDS region (P5, behind the phase's operand loads); P7's counted wait counts those 4 pieces as
+  // in flight (vmcnt(10)) and the next P3's retires them; P3 then reads them back under its MFMA cluster (the phase
+  // with the fewest fragment registers live), applies the update and stores hi / lo.  The tile's update traffic is
+  // thus spread over 16 iterations instead of arriving at once while every MFMA pipe idles.  Every slab / master
+  // address is written and read by the same lane, so program order is the only ordering needed.  The block's last
+  // tile takes the plain epilogue.  Bitwise the EPI_SGDS result (tests: test_deferred_sgd_*).
+  int dslot = -1;          // slot whose update is pending (DEFER)
+  int dm0 = 0, dn0 = 0;    // its tile origin
+  const uint32_t side_lds = (uint32_t)(uintptr_t)lds + 8 * HT + wid * 4096;
+  auto side_m = [&](int rg) { return dm0 + (rg >> 3) * 128 + wr * 64 + (rg & 3) * 16 + (lane & 15); };
+  auto side_nb = [&](int rg) { return dn0 + ((rg >> 2) & 1) * 128 + wc * 32; };
+  auto side_issue = [&](int rg) {   // P1: 4 LDS-DMA pieces of row group rg into this wave's side region
+    const GemmArgs q = reload_args();
+    DLLM_LDS char* dst = lds + 8 * HT + wid * 4096;
+    const char* slab = (const char*)(q.ws + (long)blockIdx.x * 65536);
+    glds16((const uint16_t*)(slab + ((wid * 32 + 2 * rg) * 64 + lane) * 16), dst);
+    glds16((const uint16_t*)(slab + ((wid * 32 + 2 * rg + 1) * 64 + lane) * 16), dst + 1024);
+    const long off = (long)side_m(rg);
+    const int col = side_nb(rg) + pair_col(lane);
+    glds16((const uint16_t*)q.aux_out + off * q.ldaux + col, dst + 2048);
+    glds16((const uint16_t*)q.C + off * q.ldc + col, dst + 3072);
+  };
+  uint4 sd[4];   // side data read at P3: g(nt 0), g(nt 1), hi pair, lo pair
+  auto side_read = [&]() {   // P3, issued before the MFMA cluster, waited after it
+    asm volatile("ds_read_b128 %0, %1 offset:0" : "=v"(sd[0]) : "v"(side_lds));
+    asm volatile("ds_read_b128 %0, %1 offset:1024" : "=v"(sd[1]) : "v"(side_lds));
+    asm volatile("ds_read_b128 %0, %1 offset:2048" : "=v"(sd[2]) : "v"(side_lds));
+    asm volatile("ds_read_b128 %0, %1 offset:3072" : "=v"(sd[3]) : "v"(side_lds));
+  };
+  auto side_apply = [&](int rg) {   // P3 after its MFMA cluster: the EPI_SGDS row-group update, then its 2 stores
+    const GemmArgs q = reload_args();
+    const uint4 h = pair_swap(uint2{sd[2].x, sd[2].y}, uint2{sd[2].z, sd[2].w});
+    const uint4 l = pair_swap(uint2{sd[3].x, sd[3].y}, uint2{sd[3].z, sd[3].w});
+    const f32x4_t g0 = __builtin_bit_cast(f32x4_t, sd[0]), g1 = __builtin_bit_cast(f32x4_t, sd[1]);
+    uint32_t hw[4] = {h.x, h.y, h.z, h.w}, lw[4] = {l.x, l.y, l.z, l.w};
+    const float gg[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float f0, f1;
+      split_join2(hw[j], lw[j], f0, f1);
+      f0 = __fadd_rn(f0, __fmul_rn(-q.lr, __fmul_rn(q.alpha, gg[2 * j])));
+      f1 = __fadd_rn(f1, __fmul_rn(-q.lr, __fmul_rn(q.alpha, gg[2 * j + 1])));
+      split_part2(f0, f1, hw[j], lw[j]);
+    }
+    const long off = (long)side_m(rg);
+    const int col = side_nb(rg) + pair_col(lane);
+    // inline-asm stores: hipcc would otherwise drain the whole LDS-DMA pipeline (vmcnt(0)) in front of a store to
+    // memory an in-flight side piece read; the counted waits above already order them (same lane, same address).
+    // s_nop 1 ends each: the next instruction must not overwrite the data registers before the store reads them
+    // (cdna_hip_programming.md §5.7 item 1)
+    typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
+    const u32x4_t hv = __builtin_bit_cast(u32x4_t, pair_swap(uint2{hw[0], hw[1]}, uint2{hw[2], hw[3]}));
+    const u32x4_t lv = __builtin_bit_cast(u32x4_t, pair_swap(uint2{lw[0], lw[1]}, uint2{lw[2], lw[3]}));
+    asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" :: "v"((uint16_t*)q.aux_out + off * q.ldaux + col), "v"(hv)
+                 : "memory");
+    asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" :: "v"((uint16_t*)q.C + off * q.ldc + col), "v"(lv)
+                 : "memory");
   };
   // 8-phase loop: running prefetch pointers at K-tile 2*it + 2 of the current slot; in the final iteration
   // they move to the NEXT slot's K-tile 0, so the last iteration's prefetches (K-tiles "nk", "nk+1") are
@@ -1263,6 +1329,9 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
   if (VMWAIT) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");       \
   DLLM_LDS_WAIT();                                                   \
   DLLM_BARRIER();
+    // DEFER side job of this iteration (wave-uniform): apply row group it-1 at P3, LDS-DMA row group it at P5
+    const bool side_upd = DEFER && dslot >= 0 && it >= 1 && it <= 16;
+    const bool side_dma = DEFER && dslot >= 0 && it <= 15;
     // ---- even buffer (K-tile 2it) ----
     read_a(I0{}, I0{}); read_b(I0{}, I0{}, fb0);
     stage_at(0, 1, Apf - a_kstep, 1);          // P0: A1 odd (K-tile 2it+1)
@@ -1294,8 +1363,17 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
     mfma_quad(acc[1][1], fb1);
     DLLM_BARRIER();
     stage_at(1, 1, Bpf, 0);                    // P3: B1 even
-    DLLM_PHASE_END(true)
+    DLLM_PHASE_END(true)                       // (also retires the previous iteration's P5 side pieces)
+    if constexpr (DEFER) {
+      if (side_upd) side_read();
+    }
     mfma_quad(acc[1][0], fb0);
+    if constexpr (DEFER) {
+      if (side_upd) {
+        DLLM_LDS_WAIT();
+        side_apply(it - 1);                    // 2 stores, older than P4's pieces: retired by P7's wait
+      }
+    }
     DLLM_BARRIER();
     // ---- odd buffer (K-tile 2it+1) ----
     read_a(I0{}, I1{}); read_b(I0{}, I1{}, fb0);
@@ -1306,6 +1384,9 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
     DLLM_BARRIER();
     read_b(I1{}, I1{}, fb1);
     stage_at(0, 0, Apf + a_kstep, 1);          // P5: A0 odd (K-tile 2it+3)
+    if constexpr (DEFER) {
+      if (side_dma) side_issue(it);            // 4 pieces: counted as in flight by P7, retired by the next P3
+    }
     DLLM_PHASE_END(false)
     fin_b(fb1);
     mfma_quad(acc[0][1], fb1);
@@ -1317,7 +1398,15 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
     mfma_quad(acc[1][1], fb1);
     DLLM_BARRIER();
     stage_at(1, 1, Bpf + b_kstep, 1);          // P7: B1 odd
-    DLLM_PHASE_END(true)
+    if constexpr (DEFER) {
+      // retire exactly what P0-P3 read (everything older than P5's operand pieces), not the 4 side pieces
+      if (side_dma) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      DLLM_LDS_WAIT();
+      DLLM_BARRIER();
+    } else {
+      DLLM_PHASE_END(true)
+    }
     mfma_quad(acc[1][0], fb0);
     DLLM_BARRIER();
     Apf += 2 * a_kstep;
@@ -1329,7 +1418,19 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
   // Apf/Bpf already point at its K-tile 2; this slot's epilogue runs meanwhile.  It touches no LDS and
   // has no barrier, so the (staggered) barrier sequence continues unchanged into the next slot's P0; its
   // memory operations are older than the next slot's P0-P3 stages and are retired by P3's counted wait.
-  slot_epilogue(slot, acc);
+  if constexpr (DEFER) {
+    // park the accumulators in the block's slab; the update runs under the next slot's iterations 0..16
+    const GemmArgs q = reload_args();
+    float* slab = q.ws + (long)blockIdx.x * 65536;
+#pragma unroll
+    for (int g = 0; g < 32; ++g)
+      *(f32x4_t*)(slab + ((wid * 32 + g) * 64 + lane) * 4) = acc[g >> 4][(g >> 3) & 1][(g >> 1) & 3][g & 1];
+    int sp_;
+    tile_of(q, slot, sp_, dm0, dn0);
+    dslot = slot;
+  } else {
+    slot_epilogue(slot, acc);
+  }
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -1904,6 +2005,15 @@ static void launch_8ph_act(const GemmArgs& a0, int nb0, hipStream_t s) {
   if constexpr (NPH == 8 && persistent_kernel<L, E, OutT, ACT>()) {
     GemmArgs a = a0;
     const int nb = grid_8ph(a, nb0);
+    if constexpr (L == L_TN && E == EPI_SGDS) {
+      // deferred update: a slab per block in the caller's workspace, iterations 0..16 of the next tile for the side
+      // job (nk / 2 >= 17), one tile per slot (no split-K)
+      if (a.tpb > 1 && a.ws != nullptr && a.ksplit == 1 && (long)nb * 65536 <= a.ws_numel && a.K / BT_K / 2 >= 17) {
+        hipLaunchKernelGGL((gemm_bf16_8ph<L, E, OutT, true, ACT, NPH, true, false, true>), dim3(nb), dim3(512), 0,
+                           s, a);
+        return;
+      }
+    }
     if (a.tpb > 1) {
       hipLaunchKernelGGL((gemm_bf16_8ph<L, E, OutT, true, ACT, NPH, true>), dim3(nb), dim3(512), 0, s, a);
       return;

@@ -252,6 +252,35 @@ def _splitk_counters(n: int, device: torch.device) -> torch.Tensor:
     return c
 
 
+# Deferred fused split-master SGD (csrc/gemm_kernels.h DEFER): a persistent block parks each finished tile's
+# accumulators in a 256 KiB slab and applies the update under its next tile's main loop.  Slabs: one per block of the
+# persistent grid (at most ceil(tiles / 2) + 8 blocks), cached per (device, stream).
+_DEFER = {"enabled": True}
+_SLABS: dict = {}
+
+
+def defer_slab_floats(M: int, N: int) -> int:
+    """fp32 elements of the slab workspace a deferred ``sgd_split`` GEMM with an M x N output may use."""
+    nb = (M // 256) * (N // 256)
+    return ((nb + 1) // 2 + 8) * 65536
+
+
+def _defer_workspace(numel: int, device: torch.device) -> torch.Tensor:
+    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
+    ws = _SLABS.get(key)
+    if ws is None or ws.numel() < numel:
+        ws = torch.empty(numel, dtype=torch.float32, device=device)
+        _SLABS[key] = ws
+    return ws
+
+
+def set_defer_sgd(enabled: bool) -> bool:
+    """Run the fused split-master SGD update deferred under the next tile (default) or in each tile's epilogue."""
+    old = _DEFER["enabled"]
+    _DEFER["enabled"] = bool(enabled)
+    return old
+
+
 def set_splitk_seam(enabled: bool) -> bool:
     """Combine split-K slices inside the GEMM kernel (default) or in a separate reduction pass; returns the old value."""
     old = _SEAM["enabled"]
@@ -327,6 +356,10 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
                 cnt = _splitk_counters((M // 256) * (N // 256) * 8, a.device)
         else:
             ksplit = 1
+    dws = None
+    if (epi == "sgd_split" and ksplit == 1 and _DEFER["enabled"] and K // 128 >= 17 and _POLICY["tpb"] > 1
+            and M % 256 == 0 and N % 256 == 0):
+        dws = _defer_workspace(defer_slab_floats(M, N), a.device)
     obs = _observe.active()
     if obs is not None:
         obs.gemm_begin()
@@ -339,10 +372,10 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
                      _native.stream_ptr(a.device), float(lr), float(betas[0]), float(betas[1]), float(eps),
                      float(wd), int(step), opt_m.data_ptr() if opt_m is not None else None,
                      opt_v.data_ptr() if opt_v is not None else None, ksplit,
-                     ws.data_ptr() if ws is not None else None,
+                     ws.data_ptr() if ws is not None else (dws.data_ptr() if dws is not None else None),
                      _mask_ptr(mask, M, N) if mask is not None else None,
                      BF16_VARIANTS[_VARIANT["name"]], _POLICY["tpb"], _POLICY["min_bpc"],
-                     cnt.data_ptr() if cnt is not None else None)
+                     cnt.data_ptr() if cnt is not None else None, dws.numel() if dws is not None else 0)
     _native.check(rc, f"dllm_gemm({layout},{epi},M={M},N={N},K={K})")
     if obs is not None:
         obs.gemm_end()
