@@ -142,14 +142,8 @@ def parse(argv=None):
     p.add_argument("--fp32_gemm", choices=["bf16x6", "mfma_f32"], default="bf16x6",
                    help="--dtype fp32 GEMMs: exact 3-way bf16 split on the bf16 MFMA kernels, or the fp32 MFMA kernel")
     p.add_argument("--master", choices=["split", "fp32"], default="split",
-                   help="fp32 master weights of a bf16 SGD run: split (bf16 working copy + int16 residual, exactly the "
+                   help="fp32 master weights of a bf16 run: split (bf16 working copy + int16 residual, exactly the "
                         "fp32 master, 4 B/param) or a separate fp32 buffer (6 B/param with the copy)")
-    p.add_argument("--no_defer_sgd", action="store_true",
-                   help="apply the fused split-master SGD update in each tile's epilogue instead of under the next "
-                        "tile's main loop")
-    p.add_argument("--no_splitk_seam", action="store_true",
-                   help="split-K GEMMs (small tile grids, e.g. TP shards): a separate splitk_reduce pass instead of the "
-                        "in-kernel combine")
     p.add_argument("--force_comm", action="store_true",
                    help="exercise the RCCL DDP/FSDP path of the headline at N=1 (size-1 communicators)")
     return p.parse_args(argv)
@@ -338,14 +332,6 @@ def main(argv=None) -> int:
         from dllm.ops.gemm import set_bf16_variant
 
         set_bf16_variant(a.gemm_variant)
-    if a.no_splitk_seam and not cpu:
-        from dllm.ops.gemm import set_splitk_seam
-
-        set_splitk_seam(False)
-    if a.no_defer_sgd and not cpu:
-        from dllm.ops.gemm import set_defer_sgd
-
-        set_defer_sgd(False)
     ffn = a.ffn_dim or (a.mp_ffn_dim if a.method == "tp" else 0)
     model = ModelConfig(model_size=a.model_size, ffn_dim=ffn, layers=a.layers, act=a.act, gated=a.gated)
     head = run_method(a, a.method, n, world, dev, a.steps, a.warmup, a.force_comm, model,

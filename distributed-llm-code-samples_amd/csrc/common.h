@@ -30,8 +30,9 @@ enum Layout : int { L_NT = 0, L_NN = 1, L_TN = 2 };
 //   EPI_ADAM  : same with AdamW (moments m/v share C's layout)
 //   EPI_SGDS  : EPI_SGD on a split master (below): C = the 16-bit residual plane, aux_out = the bf16 working copy
 //               (required); reads 4 B and writes 4 B per parameter instead of reading 4 B and writing 6 B
+//   EPI_ADAMS : EPI_ADAM on a split master (the moments stay fp32)
 enum Epi : int { EPI_STORE = 0, EPI_ACT = 1, EPI_DACT = 2, EPI_GLU = 3, EPI_DGLU = 4, EPI_SGD = 5, EPI_ADAM = 6,
-                 EPI_SGDS = 7 };
+                 EPI_SGDS = 7, EPI_ADAMS = 8 };
 enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_SILU = 2, ACT_GELU = 3 };
 
 __device__ __forceinline__ float bf2f(uint16_t v) {
@@ -66,6 +67,15 @@ __device__ __forceinline__ void split_part(float f, uint16_t& h, uint16_t& l) {
   const uint32_t t = __float_as_uint(f) + 0x8000u;
   h = (uint16_t)(t >> 16);
   l = (uint16_t)((t ^ 0x8000u) & 0xffffu);
+}
+
+// the AdamW update of one parameter (shared by every AdamW epilogue / kernel)
+__device__ __forceinline__ void adamw1(float& w, float& m, float& v, float g, float lr, float b1, float b2, float eps,
+                                       float wd, float bc1, float bc2) {
+  m = b1 * m + (1.f - b1) * g;
+  v = b2 * v + (1.f - b2) * g * g;
+  const float mh = m / bc1, vh = v / bc2;
+  w = w - lr * (mh / (sqrtf(vh) + eps) + wd * w);
 }
 
 __device__ __forceinline__ float act_fwd(int act, float x) {

@@ -121,6 +121,35 @@ __global__ __launch_bounds__(256) void sgd_split_kernel(uint16_t* lo, uint16_t* 
   }
 }
 
+// AdamW on a split master (moments fp32): the same update as adam_kernel, 4 B of master read + 4 B written
+__global__ __launch_bounds__(256) void adam_split_kernel(uint16_t* lo, uint16_t* hi, const void* grad, int gdt,
+                                                         float* m, float* v, long n, float lr, float b1, float b2,
+                                                         float eps, float wd, float bc1, float bc2, float gscale) {
+  const long n4 = n / 4;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    uint2 h = *(const uint2*)(hi + 4 * i), l = *(const uint2*)(lo + 4 * i);
+    f32x4_t mm = *(f32x4_t*)(m + 4 * i);
+    f32x4_t vv = *(f32x4_t*)(v + 4 * i);
+    const f32x4_t g = load_grad4(grad, gdt, 4 * i) * gscale;
+    float w[4];
+    split_join2(h.x, l.x, w[0], w[1]);
+    split_join2(h.y, l.y, w[2], w[3]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float m1 = mm[j], v1 = vv[j];
+      adamw1(w[j], m1, v1, g[j], lr, b1, b2, eps, wd, bc1, bc2);
+      mm[j] = m1;
+      vv[j] = v1;
+    }
+    split_part2(w[0], w[1], h.x, l.x);
+    split_part2(w[2], w[3], h.y, l.y);
+    *(uint2*)(hi + 4 * i) = h;
+    *(uint2*)(lo + 4 * i) = l;
+    *(f32x4_t*)(m + 4 * i) = mm;
+    *(f32x4_t*)(v + 4 * i) = vv;
+  }
+}
+
 // split master <-> fp32 (checkpoints, parameter export / import)
 __global__ __launch_bounds__(256) void split_join_kernel(const uint16_t* hi, const uint16_t* lo, float* out, long n) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
@@ -333,6 +362,15 @@ int dllm_sgd_split_step(void* lo, void* hi, const void* grad, int grad_dtype, lo
   return (int)hipGetLastError();
 }
 
+int dllm_adam_split_step(void* lo, void* hi, const void* grad, int grad_dtype, float* m, float* v, long n, float lr,
+                         float b1, float b2, float eps, float wd, int step, float gscale, void* stream) {
+  if (n % 4 || step < 1 || ((uintptr_t)lo | (uintptr_t)hi) % 8) return -1;
+  const float bc1 = 1.f - powf(b1, (float)step), bc2 = 1.f - powf(b2, (float)step);
+  hipLaunchKernelGGL(adam_split_kernel, dim3(grid_for(n / 4)), dim3(256), 0, (hipStream_t)stream, (uint16_t*)lo,
+                     (uint16_t*)hi, grad, grad_dtype, m, v, n, lr, b1, b2, eps, wd, bc1, bc2, gscale);
+  return (int)hipGetLastError();
+}
+
 // mode 0: out_f32 = join(hi, lo);  mode 1: (hi, lo) = split(in_f32)
 int dllm_split_master(void* hi, void* lo, void* f32, long n, int mode, void* stream) {
   if (n <= 0) return 0;
@@ -384,6 +422,6 @@ int dllm_occupy(int blocks, int threads, float us, float* sink, void* stream) {
   return (int)hipGetLastError();
 }
 
-int dllm_abi_version() { return 7; }
+int dllm_abi_version() { return 8; }
 
 }  // extern "C"

@@ -16,8 +16,7 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
               const void* B, long ldb, void* C, long ldc, const void* aux, void* aux_out, long ldaux,
               int M, int N, int K, float alpha, float beta, int group_m, int force_path, void* stream,
               float lr, float b1, float b2, float eps, float wd, int step, float* opt_m, float* opt_v,
-              int ksplit, float* workspace, void* mask, int variant, int tpb, int min_bpc, int* counters,
-              long ws_numel) {
+              int ksplit, float* workspace, void* mask, int variant, int tpb, int min_bpc) {
   if (M <= 0 || N <= 0 || K <= 0) return -1;
   if (layout < 0 || layout > 2) return -1;
   if ((epi == EPI_GLU || epi == EPI_DGLU) && (N % 32) != 0) return -1;
@@ -35,8 +34,6 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
   a.tpb_req = tpb;
   a.min_bpc = min_bpc < 1 ? 1 : min_bpc;
   a.ws = nullptr;
-  a.cnt = nullptr;
-  a.ws_numel = 0;
   {
     const char* sk = getenv("DLLM_PP_SKEW");
     a.skew = sk ? atoi(sk) : 0;
@@ -45,19 +42,20 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
   const bool aligned_ptr = ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && ((uintptr_t)C % 16 == 0) &&
                            ((uintptr_t)aux % 16 == 0) && ((uintptr_t)aux_out % 16 == 0) &&
                            ((uintptr_t)opt_m % 16 == 0) && ((uintptr_t)opt_v % 16 == 0);
-  const bool opt_epi = (epi == EPI_SGD || epi == EPI_ADAM || epi == EPI_SGDS);
+  const bool opt_epi = (epi == EPI_SGD || epi == EPI_ADAM || epi == EPI_SGDS || epi == EPI_ADAMS);
+  const bool split_epi = (epi == EPI_SGDS || epi == EPI_ADAMS);
   if (opt_epi && layout != L_TN) return -1;
   if ((epi == EPI_SGD || epi == EPI_ADAM) && out_dtype != DT_F32) return -1;
   // split master: C = the 16-bit residual plane, aux_out = the bf16 working copy (paired 16-B rows: ld % 8 == 0)
-  if (epi == EPI_SGDS && (out_dtype != DT_BF16 || in_dtype != DT_BF16 || aux_out == nullptr)) return -1;
-  if (epi == EPI_ADAM) {
+  if (split_epi && (out_dtype != DT_BF16 || in_dtype != DT_BF16 || aux_out == nullptr)) return -1;
+  if (epi == EPI_ADAM || epi == EPI_ADAMS) {
     if (step < 1 || !opt_m || !opt_v) return -1;
     a.bc1 = 1.f - powf(b1, (float)step);
     a.bc2 = 1.f - powf(b2, (float)step);
   }
   int path = 2;
   const bool aligned_lds = aligned_ptr && (lda % 8 == 0) && (ldb % 8 == 0) && (ldc % 4 == 0) && (ldaux % 4 == 0) &&
-                           (epi != EPI_SGDS || (ldc % 8 == 0 && ldaux % 8 == 0));
+                           (!split_epi || (ldc % 8 == 0 && ldaux % 8 == 0));
   if (in_dtype == DT_BF16 && M % BT_M == 0 && N % BT_N == 0 && K % BT_K == 0 && aligned_lds) path = 0;
   if (in_dtype == DT_F32 && out_dtype == DT_F32 && M % FT == 0 && N % FT == 0 && K % FK == 0 && aligned_lds) path = 1;
   if (force_path >= 0) {
@@ -66,11 +64,6 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
     path = force_path;
   }
   if (path == 2 && epi == EPI_GLU && aux_out == nullptr) return -1;
-  if (epi == EPI_SGDS && ksplit <= 1 && workspace != nullptr && ws_numel > 0) {
-    // deferred fused update (persistent 8-phase grids): the workspace holds one 256 KiB slab per block
-    a.ws = workspace;
-    a.ws_numel = ws_numel;
-  }
   if (ksplit > 1) {
     // split-K only on the bf16 8-phase path (each slice an even number of 64-deep K-tiles); a request
     // that cannot be honoured (other kernel family / forced 2-stage variant) runs unsplit
@@ -78,7 +71,6 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
     if (path == 0 && (K / BT_K) % (2 * ksplit) == 0 && a.variant != 1) {
       a.ksplit = ksplit;
       a.ws = workspace;
-      a.cnt = counters;  // (M/256)*(N/256)*8 zeroed ints: combine in the kernel; null: a splitk_reduce pass
     }
   }
   if (mask != nullptr) {

@@ -78,10 +78,6 @@ struct GemmArgs {
   // gemm_bf16_pp: initial delay (x 64 clocks) of the odd workgroup slot of each CU, so the two co-resident blocks
   // start out of phase (experiment knob, DLLM_PP_SKEW; 0 = none)
   int skew;
-  // in-kernel split-K combine (SEAM instantiations): per (tile, wave) arrival counters, zero at launch and left zero
-  // by each tile's last arriver; ws then holds the per-slice partials in the accumulator-native layout
-  int* cnt;
-  long ws_numel;  // floats available at ws (DEFER slabs: 65536 per block)
 };
 
 // ----------------------------------------------------------------------------------------------
@@ -165,6 +161,26 @@ __device__ __forceinline__ void epi4(const GemmArgs& p, int m, int n, f32x4_t v)
     split_part2(w[2], w[3], h.y, l.y);
     *hp = h;
     *lp = l;
+  } else if constexpr (EPI == EPI_ADAMS) {
+    uint2* hp = (uint2*)((uint16_t*)p.aux_out + (long)m * p.ldaux + n);
+    uint2* lp = (uint2*)((uint16_t*)p.C + ci);
+    uint2 h = *hp, l = *lp;
+    f32x4_t mm = Vec4<float>::load(p.opt_m, ci), vv = Vec4<float>::load(p.opt_v, ci);
+    float w[4];
+    split_join2(h.x, l.x, w[0], w[1]);
+    split_join2(h.y, l.y, w[2], w[3]);
+    for (int r = 0; r < 4; ++r) {
+      float m1 = mm[r], v1 = vv[r];
+      adamw1(w[r], m1, v1, p.alpha * v[r], p.lr, p.b1, p.b2, p.eps, p.wd, p.bc1, p.bc2);
+      mm[r] = m1;
+      vv[r] = v1;
+    }
+    split_part2(w[0], w[1], h.x, l.x);
+    split_part2(w[2], w[3], h.y, l.y);
+    *hp = h;
+    *lp = l;
+    Vec4<float>::store(p.opt_m, ci, mm);
+    Vec4<float>::store(p.opt_v, ci, vv);
   } else if constexpr (EPI == EPI_ADAM) {
     f32x4_t w = Vec4<float>::load(p.C, ci);
     f32x4_t mm = Vec4<float>::load(p.opt_m, ci);
@@ -290,7 +306,7 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
   // (the beta != 0 store path is off the FFN hot path: small batches keep the persistent kernel's
   // in-loop epilogue within the register budget)
   constexpr int COST = EPI == EPI_DACT ? WR : EPI == EPI_DGLU ? 8 * (BF ? 2 : 4) : EPI == EPI_STORE ? 4 * WR
-                     : EPI == EPI_SGD || EPI == EPI_SGDS ? 8 : EPI == EPI_ADAM ? 24 : 0;
+                     : EPI == EPI_SGD || EPI == EPI_SGDS ? 8 : EPI == EPI_ADAM || EPI == EPI_ADAMS ? 24 : 0;
   constexpr int RB = epi_batch(COST);
   const int pc = pair_col(lane);
 #define DLLM_M(rg) (m0 + ((rg) >> 3) * 128 + wr * 64 + ((rg) & 3) * 16 + (lane & 15))
@@ -557,6 +573,56 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
             pair_swap(uint2{hw[0], hw[1]}, uint2{hw[2], hw[3]});
         *(uint4*)((uint16_t*)Cp + (long)DLLM_M(b0 + r) * p.ldc + DLLM_NB(b0 + r) + pc) =
             pair_swap(uint2{lw[0], lw[1]}, uint2{lw[2], lw[3]});
+      }
+    }
+  } else if constexpr (EPI == EPI_ADAMS) {
+    // split master + fp32 moments: per row group one paired 16-B access per plane and two 16-B moment accesses per
+    // fragment (24 B per parameter instead of 26 B)
+#pragma unroll
+    for (int b0 = 0; b0 < 16; b0 += RB) {
+      uint4 H[RB], Lw[RB];
+      f32x4_t Mm[RB][2], Vv[RB][2];
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        H[r] = *(const uint4*)((const uint16_t*)p.aux_out + (long)DLLM_M(b0 + r) * p.ldaux + DLLM_NB(b0 + r) + pc);
+        Lw[r] = *(const uint4*)((const uint16_t*)Cp + (long)DLLM_M(b0 + r) * p.ldc + DLLM_NB(b0 + r) + pc);
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const long ci = (long)DLLM_M(b0 + r) * p.ldc + DLLM_N(b0 + r, nt);
+          Mm[r][nt] = RF::load(p.opt_m, ci);
+          Vv[r][nt] = RF::load(p.opt_v, ci);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        const uint4 h = pair_swap(uint2{H[r].x, H[r].y}, uint2{H[r].z, H[r].w});
+        const uint4 l = pair_swap(uint2{Lw[r].x, Lw[r].y}, uint2{Lw[r].z, Lw[r].w});
+        uint32_t hw[4] = {h.x, h.y, h.z, h.w}, lw[4] = {l.x, l.y, l.z, l.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int nt = j >> 1, e = 2 * (j & 1);
+          const f32x4_t gg = DLLM_ACC(b0 + r, nt);
+          float f0, f1;
+          split_join2(hw[j], lw[j], f0, f1);
+          float m0 = Mm[r][nt][e], v0 = Vv[r][nt][e], m1 = Mm[r][nt][e + 1], v1 = Vv[r][nt][e + 1];
+          adamw1(f0, m0, v0, p.alpha * gg[e], p.lr, p.b1, p.b2, p.eps, p.wd, p.bc1, p.bc2);
+          adamw1(f1, m1, v1, p.alpha * gg[e + 1], p.lr, p.b1, p.b2, p.eps, p.wd, p.bc1, p.bc2);
+          Mm[r][nt][e] = m0;
+          Vv[r][nt][e] = v0;
+          Mm[r][nt][e + 1] = m1;
+          Vv[r][nt][e + 1] = v1;
+          split_part2(f0, f1, hw[j], lw[j]);
+        }
+        *(uint4*)((uint16_t*)p.aux_out + (long)DLLM_M(b0 + r) * p.ldaux + DLLM_NB(b0 + r) + pc) =
+            pair_swap(uint2{hw[0], hw[1]}, uint2{hw[2], hw[3]});
+        *(uint4*)((uint16_t*)Cp + (long)DLLM_M(b0 + r) * p.ldc + DLLM_NB(b0 + r) + pc) =
+            pair_swap(uint2{lw[0], lw[1]}, uint2{lw[2], lw[3]});
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const long ci = (long)DLLM_M(b0 + r) * p.ldc + DLLM_N(b0 + r, nt);
+          Vec4<float>::store(p.opt_m, ci, Mm[r][nt]);
+          Vec4<float>::store(p.opt_v, ci, Vv[r][nt]);
+        }
       }
     }
   } else if constexpr (EPI == EPI_ADAM && DLLM_ADAM_PIPE) {
@@ -902,86 +968,15 @@ __device__ __forceinline__ GemmArgs reload_args() {
     __builtin_amdgcn_sched_barrier(0);                    \
   } while (0)
 
-// In-kernel split-K combine (the SEAM instantiations of gemm_bf16_8ph; replaces the separate splitk_reduce pass).
-// Every wave of every K-slice block stores its fp32 partial -- 32 x 16 B per lane, lane-interleaved, so each store
-// instruction writes 1 KB contiguous -- write-through (sc1), drains it (vmcnt(0)) and takes a ticket on its own
-// (tile, wave) counter (relaxed agent-scope atomic).  The wave that draws ksplit - 1 is the last arriver: it reads
-// all ksplit partials back with sc1 loads (they bypass this CU's L1 and the other XCDs' L2s hold none of them: no
-// acquire fence), sums them in slice order from zero -- the splitk_reduce order, so the result does not depend on
-// which slice arrives last -- resets the counter, and runs the real epilogue for its 128x64 region.  Nothing waits
-// on another block, so the protocol cannot hang, and one wave's hand-off needs no workgroup barrier (the staggered
-// wave groups of the 8-phase schedule never meet at one).  cdna_hip_programming.md §5 "Projection GEMM" item 2 and
-// §6 Guideline 16 (sc1 slab stores, relaxed agent ticket, sc1 slab loads).
-// last arriver: ac = sum of the S partials in slice order, from zero.  All S slices of a batch of CG accumulator
-// groups are loaded before any is added (S * CG * 4 <= 64 VGPRs in flight: the fragment registers are dead here), so
-// the combine costs 32 / CG memory round trips, not 32 * S.  Fully unrolled: ac is never indexed at run time.
-template <int S>
-__device__ __forceinline__ void seam_sum(f32x4_t (&ac)[2][2][4][2], __amdgpu_buffer_rsrc_t rs, int wid, int lane) {
-  constexpr int CG = 16 / S >= 8 ? 8 : 16 / S >= 4 ? 4 : 16 / S >= 2 ? 2 : 1;
-#pragma unroll
-  for (int g0 = 0; g0 < 32; g0 += CG) {
-    f32x4_t t[S][CG];
-#pragma unroll
-    for (int sl = 0; sl < S; ++sl)
-#pragma unroll
-      for (int j = 0; j < CG; ++j)
-        t[sl][j] = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
-                                                   rs, ((sl * 8 + wid) * 32 + g0 + j) * 1024 + lane * 16, 0, 16));
-#pragma unroll
-    for (int j = 0; j < CG; ++j) {
-      const int g = g0 + j;
-      f32x4_t v = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int sl = 0; sl < S; ++sl) v += t[sl][j];
-      ac[g >> 4][(g >> 3) & 1][(g >> 1) & 3][g & 1] = v;
-    }
-  }
-}
-
-template <int EPI, typename OutT, int ACT>
-__device__ __forceinline__ void seam_epilogue(const GemmArgs& q, f32x4_t (&ac)[2][2][4][2], int sp, int tm0,
-                                              int tn0, int wr, int wc, int wid, int lane) {
-  typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
-  const int S = q.ksplit;
-  const int tile = (tm0 / BT_M) * (q.N / BT_N) + tn0 / BT_N;
-  // [tile][slice][wave][32 groups][64 lanes] x 16 B; one buffer resource per tile (S * 256 KiB < 2^31)
-  const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc(q.ws + (long)tile * S * 65536, (short)0, S * 65536 * 4, 0x00020000);
-  const int own = ((sp * 8 + wid) * 32) * 1024 + lane * 16;
-#pragma unroll
-  for (int g = 0; g < 32; ++g)
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, ac[g >> 4][(g >> 3) & 1][(g >> 1) & 3][g & 1]),
-                                           rs, own + g * 1024, 0, 16 /* sc1 */);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial is in memory before its ticket
-  int* c = q.cnt + tile * 8 + wid;
-  int ticket = 0;
-  if (lane == 0) ticket = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  ticket = __builtin_amdgcn_readfirstlane(ticket);
-  if (ticket != S - 1) return;
-  if (lane == 0) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: keep the loads below the ticket
-  switch (S) {
-    case 2: seam_sum<2>(ac, rs, wid, lane); break;
-    case 3: seam_sum<3>(ac, rs, wid, lane); break;
-    case 4: seam_sum<4>(ac, rs, wid, lane); break;
-    case 6: seam_sum<6>(ac, rs, wid, lane); break;
-    default: seam_sum<8>(ac, rs, wid, lane); break;  // the host splits K by 2, 3, 4, 6 or 8 only
-  }
-  epilogue_256<EPI, OutT, ACT>(q, ac, tm0, tn0, wr, wc, lane, q.C);
-}
-
 // ACT >= 0: activation of the ACT/DACT/GLU/DGLU epilogues fixed at compile time (-1: runtime p.act)
 // NPH = 8: the 8-phase schedule below (one quadrant = 16 MFMAs per wave per barrier interval).
 // NPH = 4: half-tile phases (two quadrants = 32 MFMAs per interval, two half-tiles restaged per phase):
 // halves the barrier count per MFMA (see the NPH == 4 loop).
-// SEAM: split-K slices combined in the kernel (seam_epilogue); p.ksplit > 1, p.ws / p.cnt set, one slot per block.
-// DEFER (persistent EPI_SGDS only): a tile's optimizer update runs under the NEXT tile's main loop (see below).
-template <int LAYOUT, int EPI, typename OutT, bool STAGGER, int ACT = -1, int NPH = 8, bool PERS = false,
-          bool SEAM = false, bool DEFER = false>
+template <int LAYOUT, int EPI, typename OutT, bool STAGGER, int ACT = -1, int NPH = 8, bool PERS = false>
 __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
   // slot(op, hh, buf) = ((op*2 + hh)*2 + buf) * 16 KiB: A in [0, 64K), B in [64K, 128K), so every
-  // fragment read is base + a 16-bit immediate.  DEFER adds a 32 KiB side region at 128K (4 KiB per wave).
-  __shared__ __attribute__((aligned(16))) char smem[8 * HT + (DEFER ? 32768 : 0)];
+  // fragment read is base + a 16-bit immediate
+  __shared__ __attribute__((aligned(16))) char smem[8 * HT];
   DLLM_LDS char* lds = (DLLM_LDS char*)smem;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1037,10 +1032,6 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
     const GemmArgs q = reload_args();
     int sp, tm0, tn0;
     tile_of(q, s, sp, tm0, tn0);
-    if constexpr (SEAM) {
-      seam_epilogue<EPI, OutT, ACT>(q, ac, sp, tm0, tn0, wr, wc, wid, lane);
-      return;
-    }
     void* out = q.C;
     if constexpr (EPI == EPI_STORE)
       if (q.ksplit > 1) out = (char*)q.C + (long)sp * q.M * q.ldc * sizeof(OutT);
@@ -1058,70 +1049,6 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
     const uint32_t* off = op == 0 ? aoff : boff;
     glds16((const uint16_t*)((const char*)src + off[0]), dst + wid * 1024);
     glds16((const uint16_t*)((const char*)src + off[1]), dst + (wid + 8) * 1024);
-  };
-
-  // ---- DEFER: the fused split-master SGD update of a tile, spread over the next tile's main loop ----
-  // A persistent block that has another tile to run does not update the master at the end of a tile: each thread
-  // stores its 128 fp32 accumulators to the block's scratch slab (p.ws, 256 KiB per block, lane-interleaved so every
-  // store instruction writes 1 KiB) and moves on.  During the next tile's iterations 0..15 every wave LDS-DMAs one
-  // row group's worth -- its two accumulator groups from the slab, the paired hi / lo words of the master -- into its
-  // own 4 KiB of a side LDS region (P5, behind the phase's operand loads); P7's counted wait counts those 4 pieces as
-  // in flight (vmcnt(10)) and the next P3's retires them; P3 then reads them back under its MFMA cluster (the phase
-  // with the fewest fragment registers live), applies the update and stores hi / lo.  The tile's update traffic is
-  // thus spread over 16 iterations instead of arriving at once while every MFMA pipe idles.  Every slab / master
-  // address is written and read by the same lane, so program order is the only ordering needed.  The block's last
-  // tile takes the plain epilogue.  Bitwise the EPI_SGDS result (tests: test_deferred_sgd_*).
-  int dslot = -1;          // slot whose update is pending (DEFER)
-  int dm0 = 0, dn0 = 0;    // its tile origin
-  const uint32_t side_lds = (uint32_t)(uintptr_t)lds + 8 * HT + wid * 4096;
-  auto side_m = [&](int rg) { return dm0 + (rg >> 3) * 128 + wr * 64 + (rg & 3) * 16 + (lane & 15); };
-  auto side_nb = [&](int rg) { return dn0 + ((rg >> 2) & 1) * 128 + wc * 32; };
-  auto side_issue = [&](int rg) {   // P1: 4 LDS-DMA pieces of row group rg into this wave's side region
-    const GemmArgs q = reload_args();
-    DLLM_LDS char* dst = lds + 8 * HT + wid * 4096;
-    const char* slab = (const char*)(q.ws + (long)blockIdx.x * 65536);
-    glds16((const uint16_t*)(slab + ((wid * 32 + 2 * rg) * 64 + lane) * 16), dst);
-    glds16((const uint16_t*)(slab + ((wid * 32 + 2 * rg + 1) * 64 + lane) * 16), dst + 1024);
-    const long off = (long)side_m(rg);
-    const int col = side_nb(rg) + pair_col(lane);
-    glds16((const uint16_t*)q.aux_out + off * q.ldaux + col, dst + 2048);
-    glds16((const uint16_t*)q.C + off * q.ldc + col, dst + 3072);
-  };
-  uint4 sd[4];   // side data read at P3: g(nt 0), g(nt 1), hi pair, lo pair
-  auto side_read = [&]() {   // P3, issued before the MFMA cluster, waited after it
-    asm volatile("ds_read_b128 %0, %1 offset:0" : "=v"(sd[0]) : "v"(side_lds));
-    asm volatile("ds_read_b128 %0, %1 offset:1024" : "=v"(sd[1]) : "v"(side_lds));
-    asm volatile("ds_read_b128 %0, %1 offset:2048" : "=v"(sd[2]) : "v"(side_lds));
-    asm volatile("ds_read_b128 %0, %1 offset:3072" : "=v"(sd[3]) : "v"(side_lds));
-  };
-  auto side_apply = [&](int rg) {   // P3 after its MFMA cluster: the EPI_SGDS row-group update, then its 2 stores
-    const GemmArgs q = reload_args();
-    const uint4 h = pair_swap(uint2{sd[2].x, sd[2].y}, uint2{sd[2].z, sd[2].w});
-    const uint4 l = pair_swap(uint2{sd[3].x, sd[3].y}, uint2{sd[3].z, sd[3].w});
-    const f32x4_t g0 = __builtin_bit_cast(f32x4_t, sd[0]), g1 = __builtin_bit_cast(f32x4_t, sd[1]);
-    uint32_t hw[4] = {h.x, h.y, h.z, h.w}, lw[4] = {l.x, l.y, l.z, l.w};
-    const float gg[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float f0, f1;
-      split_join2(hw[j], lw[j], f0, f1);
-      f0 = __fadd_rn(f0, __fmul_rn(-q.lr, __fmul_rn(q.alpha, gg[2 * j])));
-      f1 = __fadd_rn(f1, __fmul_rn(-q.lr, __fmul_rn(q.alpha, gg[2 * j + 1])));
-      split_part2(f0, f1, hw[j], lw[j]);
-    }
-    const long off = (long)side_m(rg);
-    const int col = side_nb(rg) + pair_col(lane);
-    // inline-asm stores: hipcc would otherwise drain the whole LDS-DMA pipeline (vmcnt(0)) in front of a store to
-    // memory an in-flight side piece read; the counted waits above already order them (same lane, same address).
-    // s_nop 1 ends each: the next instruction must not overwrite the data registers before the store reads them
-    // (cdna_hip_programming.md §5.7 item 1)
-    typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
-    const u32x4_t hv = __builtin_bit_cast(u32x4_t, pair_swap(uint2{hw[0], hw[1]}, uint2{hw[2], hw[3]}));
-    const u32x4_t lv = __builtin_bit_cast(u32x4_t, pair_swap(uint2{lw[0], lw[1]}, uint2{lw[2], lw[3]}));
-    asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" :: "v"((uint16_t*)q.aux_out + off * q.ldaux + col), "v"(hv)
-                 : "memory");
-    asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" :: "v"((uint16_t*)q.C + off * q.ldc + col), "v"(lv)
-                 : "memory");
   };
   // 8-phase loop: running prefetch pointers at K-tile 2*it + 2 of the current slot; in the final iteration
   // they move to the NEXT slot's K-tile 0, so the last iteration's prefetches (K-tiles "nk", "nk+1") are
@@ -1329,9 +1256,6 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
   if (VMWAIT) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");       \
   DLLM_LDS_WAIT();                                                   \
   DLLM_BARRIER();
-    // DEFER side job of this iteration (wave-uniform): apply row group it-1 at P3, LDS-DMA row group it at P5
-    const bool side_upd = DEFER && dslot >= 0 && it >= 1 && it <= 16;
-    const bool side_dma = DEFER && dslot >= 0 && it <= 15;
     // ---- even buffer (K-tile 2it) ----
     read_a(I0{}, I0{}); read_b(I0{}, I0{}, fb0);
     stage_at(0, 1, Apf - a_kstep, 1);          // P0: A1 odd (K-tile 2it+1)
@@ -1363,17 +1287,8 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
     mfma_quad(acc[1][1], fb1);
     DLLM_BARRIER();
     stage_at(1, 1, Bpf, 0);                    // P3: B1 even
-    DLLM_PHASE_END(true)                       // (also retires the previous iteration's P5 side pieces)
-    if constexpr (DEFER) {
-      if (side_upd) side_read();
-    }
+    DLLM_PHASE_END(true)
     mfma_quad(acc[1][0], fb0);
-    if constexpr (DEFER) {
-      if (side_upd) {
-        DLLM_LDS_WAIT();
-        side_apply(it - 1);                    // 2 stores, older than P4's pieces: retired by P7's wait
-      }
-    }
     DLLM_BARRIER();
     // ---- odd buffer (K-tile 2it+1) ----
     read_a(I0{}, I1{}); read_b(I0{}, I1{}, fb0);
@@ -1384,9 +1299,6 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
     DLLM_BARRIER();
     read_b(I1{}, I1{}, fb1);
     stage_at(0, 0, Apf + a_kstep, 1);          // P5: A0 odd (K-tile 2it+3)
-    if constexpr (DEFER) {
-      if (side_dma) side_issue(it);            // 4 pieces: counted as in flight by P7, retired by the next P3
-    }
     DLLM_PHASE_END(false)
     fin_b(fb1);
     mfma_quad(acc[0][1], fb1);
@@ -1398,15 +1310,7 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
     mfma_quad(acc[1][1], fb1);
     DLLM_BARRIER();
     stage_at(1, 1, Bpf + b_kstep, 1);          // P7: B1 odd
-    if constexpr (DEFER) {
-      // retire exactly what P0-P3 read (everything older than P5's operand pieces), not the 4 side pieces
-      if (side_dma) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      DLLM_LDS_WAIT();
-      DLLM_BARRIER();
-    } else {
-      DLLM_PHASE_END(true)
-    }
+    DLLM_PHASE_END(true)
     mfma_quad(acc[1][0], fb0);
     DLLM_BARRIER();
     Apf += 2 * a_kstep;
@@ -1418,19 +1322,7 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
   // Apf/Bpf already point at its K-tile 2; this slot's epilogue runs meanwhile.  It touches no LDS and
   // has no barrier, so the (staggered) barrier sequence continues unchanged into the next slot's P0; its
   // memory operations are older than the next slot's P0-P3 stages and are retired by P3's counted wait.
-  if constexpr (DEFER) {
-    // park the accumulators in the block's slab; the update runs under the next slot's iterations 0..16
-    const GemmArgs q = reload_args();
-    float* slab = q.ws + (long)blockIdx.x * 65536;
-#pragma unroll
-    for (int g = 0; g < 32; ++g)
-      *(f32x4_t*)(slab + ((wid * 32 + g) * 64 + lane) * 4) = acc[g >> 4][(g >> 3) & 1][(g >> 1) & 3][g & 1];
-    int sp_;
-    tile_of(q, slot, sp_, dm0, dn0);
-    dslot = slot;
-  } else {
-    slot_epilogue(slot, acc);
-  }
+  slot_epilogue(slot, acc);
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -1784,6 +1676,15 @@ __global__ __launch_bounds__(256) void gemm_generic(GemmArgs p) {
         uint16_t* lp = (uint16_t*)p.C + (long)m * p.ldc + n;
         const float w = __fadd_rn(split_join(*hp, *lp), __fmul_rn(-p.lr, __fmul_rn(p.alpha, v)));
         split_part(w, *hp, *lp);
+      } else if constexpr (EPI == EPI_ADAMS) {
+        const long ci = (long)m * p.ldc + n;
+        uint16_t* hp = (uint16_t*)p.aux_out + (long)m * p.ldaux + n;
+        uint16_t* lp = (uint16_t*)p.C + ci;
+        float w = split_join(*hp, *lp), mm = p.opt_m[ci], vv = p.opt_v[ci];
+        adamw1(w, mm, vv, p.alpha * v, p.lr, p.b1, p.b2, p.eps, p.wd, p.bc1, p.bc2);
+        split_part(w, *hp, *lp);
+        p.opt_m[ci] = mm;
+        p.opt_v[ci] = vv;
       } else if constexpr (EPI == EPI_ADAM) {
         const long ci = (long)m * p.ldc + n;
         float* W = (float*)p.C;
@@ -1947,21 +1848,9 @@ static void launch_pp(const GemmArgs& a, hipStream_t s) {
   launch_pp_act<L, E, OutT, -1>(a, s);
 }
 
-// main kernel writes partials into the workspace, then the reduction applies the epilogue -- or, with arrival
-// counters (a.cnt) on the 8-phase family, the slices combine inside the kernel (SEAM, no second pass)
+// main kernel writes partials into the workspace, then the reduction applies the epilogue
 template <int L, int E>
 static hipError_t launch_splitk(const GemmArgs& a, int out_dt, float* ws, hipStream_t s) {
-  if (a.cnt != nullptr && a.variant != 4 && a.variant != 5) {
-    GemmArgs w = a;
-    w.ws = ws;
-    w.tpb = 1;
-    const int nb = (a.M / BT_M) * (a.N / BT_N) * a.ksplit;
-    if (out_dt == DT_F32)
-      hipLaunchKernelGGL((gemm_bf16_8ph<L, E, float, true, -1, 8, false, true>), dim3(nb), dim3(512), 0, s, w);
-    else
-      hipLaunchKernelGGL((gemm_bf16_8ph<L, E, uint16_t, true, -1, 8, false, true>), dim3(nb), dim3(512), 0, s, w);
-    return hipGetLastError();
-  }
   GemmArgs w = a;
   w.C = ws;
   w.ldc = a.N;
@@ -2005,15 +1894,6 @@ static void launch_8ph_act(const GemmArgs& a0, int nb0, hipStream_t s) {
   if constexpr (NPH == 8 && persistent_kernel<L, E, OutT, ACT>()) {
     GemmArgs a = a0;
     const int nb = grid_8ph(a, nb0);
-    if constexpr (L == L_TN && E == EPI_SGDS) {
-      // deferred update: a slab per block in the caller's workspace, iterations 0..16 of the next tile for the side
-      // job (nk / 2 >= 17), one tile per slot (no split-K)
-      if (a.tpb > 1 && a.ws != nullptr && a.ksplit == 1 && (long)nb * 65536 <= a.ws_numel && a.K / BT_K / 2 >= 17) {
-        hipLaunchKernelGGL((gemm_bf16_8ph<L, E, OutT, true, ACT, NPH, true, false, true>), dim3(nb), dim3(512), 0,
-                           s, a);
-        return;
-      }
-    }
     if (a.tpb > 1) {
       hipLaunchKernelGGL((gemm_bf16_8ph<L, E, OutT, true, ACT, NPH, true>), dim3(nb), dim3(512), 0, s, a);
       return;
@@ -2124,7 +2004,7 @@ static hipError_t dispatch_opt(int path, const GemmArgs& a, int in_dt, hipStream
     return hipGetLastError();
   }
   dim3 grid((a.N + 63) / 64, (a.M + 63) / 64);
-  if constexpr (E == EPI_SGDS) {  // split masters exist only next to a bf16 working copy: bf16 inputs
+  if constexpr (E == EPI_SGDS || E == EPI_ADAMS) {  // split masters exist only next to a bf16 working copy
     if (path == 1 || in_dt != DT_BF16) return hipErrorInvalidValue;
     hipLaunchKernelGGL((gemm_generic<L_TN, E, uint16_t, float>), grid, dim3(256), 0, s, a);
   } else {

@@ -11,6 +11,7 @@ hipError_t dispatch_tn(int path, int epi, const GemmArgs& a, int in_dt, int out_
 hipError_t dispatch_tn_opt(int path, int epi, const GemmArgs& a, int in_dt, hipStream_t s) {
   if (epi == EPI_SGD) return dispatch_opt<EPI_SGD>(path, a, in_dt, s);
   if (epi == EPI_SGDS) return dispatch_opt<EPI_SGDS>(path, a, in_dt, s);
+  if (epi == EPI_ADAMS) return dispatch_opt<EPI_ADAMS>(path, a, in_dt, s);
   return dispatch_opt<EPI_ADAM>(path, a, in_dt, s);
 }
 

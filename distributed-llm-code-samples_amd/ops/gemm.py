@@ -20,6 +20,7 @@ followed by an epilogue:
 * ``"adam"``:  same with fused AdamW; ``opt_m``/``opt_v`` share ``C``'s layout
 * ``"sgd_split"``: ``"sgd"`` on a split master (``ops/master.py``): ``C`` is the int16 residual plane, ``aux_out``
   (required) the bf16 working copy; together they hold the fp32 master, updated exactly as ``"sgd"`` updates it
+* ``"adam_split"``: ``"adam"`` on a split master (fp32 moments ``opt_m``/``opt_v`` in ``C``'s layout)
 
 CUDA (HIP) tensors run the hand-written gfx950 kernels of ``csrc/gemm_kernels.h``; CPU tensors run the torch
 reference below (used by the CPU/gloo tests and as the numerics oracle).  There is no silent fallback:
@@ -35,7 +36,7 @@ from .activations import act_code, act_fwd, act_grad
 from .master import join_master, set_master_
 
 LAYOUTS = {"nt": 0, "nn": 1, "tn": 2}
-EPIS = {"store": 0, "act": 1, "dact": 2, "glu": 3, "dglu": 4, "sgd": 5, "adam": 6, "sgd_split": 7}
+EPIS = {"store": 0, "act": 1, "dact": 2, "glu": 3, "dglu": 4, "sgd": 5, "adam": 6, "sgd_split": 7, "adam_split": 8}
 FORCE = {None: -1, "mfma_bf16": 0, "mfma_f32": 1, "generic": 2, "bf16x6": -1}
 
 
@@ -116,6 +117,11 @@ def _torch_gemm(a, b, layout, out, epi, act, aux, aux_out, alpha, beta, opt=None
         w = join_master(aux_out, out)
         w.add_(-opt["lr"] * (alpha * acc).to(torch.float32))
         set_master_(aux_out, out, w)
+    elif epi == "adam_split":
+        w = join_master(aux_out, out)
+        _torch_gemm(a, b, layout, w, "adam", act, aux, None, alpha, beta, opt)
+        set_master_(aux_out, out, w)
+        return out
     elif epi == "adam":
         g = (alpha * acc).to(out.dtype)
         b1, b2, step = opt["b1"], opt["b2"], opt["step"]
@@ -236,58 +242,6 @@ def _splitk_workspace(numel: int, device: torch.device) -> torch.Tensor:
     return ws
 
 
-# In-kernel split-K combine (csrc/gemm_kernels.h seam_epilogue): per (tile, wave) arrival counters, zeroed once here;
-# every launch leaves them zero again (each tile's last arriver resets its counter), so no per-call memset.  Cached per
-# (device, stream) like the partial workspace.  _SEAM["enabled"] False: the separate splitk_reduce pass instead.
-_CNT: dict = {}
-_SEAM = {"enabled": True}
-
-
-def _splitk_counters(n: int, device: torch.device) -> torch.Tensor:
-    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
-    c = _CNT.get(key)
-    if c is None or c.numel() < n:
-        c = torch.zeros(n, dtype=torch.int32, device=device)
-        _CNT[key] = c
-    return c
-
-
-# Deferred fused split-master SGD (csrc/gemm_kernels.h DEFER): a persistent block parks each finished tile's
-# accumulators in a 256 KiB slab and applies the update under its next tile's main loop.  Slabs: one per block of the
-# persistent grid (at most ceil(tiles / 2) + 8 blocks), cached per (device, stream).
-_DEFER = {"enabled": True}
-_SLABS: dict = {}
-
-
-def defer_slab_floats(M: int, N: int) -> int:
-    """fp32 elements of the slab workspace a deferred ``sgd_split`` GEMM with an M x N output may use."""
-    nb = (M // 256) * (N // 256)
-    return ((nb + 1) // 2 + 8) * 65536
-
-
-def _defer_workspace(numel: int, device: torch.device) -> torch.Tensor:
-    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
-    ws = _SLABS.get(key)
-    if ws is None or ws.numel() < numel:
-        ws = torch.empty(numel, dtype=torch.float32, device=device)
-        _SLABS[key] = ws
-    return ws
-
-
-def set_defer_sgd(enabled: bool) -> bool:
-    """Run the fused split-master SGD update deferred under the next tile (default) or in each tile's epilogue."""
-    old = _DEFER["enabled"]
-    _DEFER["enabled"] = bool(enabled)
-    return old
-
-
-def set_splitk_seam(enabled: bool) -> bool:
-    """Combine split-K slices inside the GEMM kernel (default) or in a separate reduction pass; returns the old value."""
-    old = _SEAM["enabled"]
-    _SEAM["enabled"] = bool(enabled)
-    return old
-
-
 def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None = None, *, epi: str = "store",
          act: str = "none", aux: torch.Tensor | None = None, aux_out: torch.Tensor | None = None,
          alpha: float = 1.0, beta: float = 0.0, out_dtype: torch.dtype | None = None, group_m: int = 4,
@@ -317,10 +271,12 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
         for t in (opt_m, opt_v):
             if t is not None and (t.shape != out.shape or t.stride() != out.stride()):
                 raise ValueError("optimizer moments must share the master weight's layout")
-    if epi == "sgd_split":
+    if epi in ("sgd_split", "adam_split"):
+        if epi == "adam_split" and (opt_m is None or opt_v is None or step < 1):
+            raise ValueError("adam_split epilogue needs opt_m, opt_v and step >= 1")
         if layout != "tn" or out.dtype != torch.int16 or aux_out is None or aux_out.dtype != torch.bfloat16 \
                 or aux_out.shape != out.shape or a.dtype != torch.bfloat16:
-            raise ValueError("sgd_split needs the TN layout, bf16 operands, an int16 residual plane as out and its "
+            raise ValueError(f"{epi} needs the TN layout, bf16 operands, an int16 residual plane as out and its "
                              "bf16 working copy as aux_out")
     if a.device.type != "cuda":
         opt = {"lr": lr, "b1": betas[0], "b2": betas[1], "eps": eps, "wd": wd, "step": step, "m": opt_m, "v": opt_v}
@@ -339,7 +295,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
     auxt = aux if aux is not None else aux_out
     if auxt is not None:
         _check_rowmajor(auxt, "aux")
-        if epi in ("sgd", "adam", "sgd_split"):
+        if epi in ("sgd", "adam", "sgd_split", "adam_split"):
             if auxt.dtype != torch.bfloat16 or auxt.shape != out.shape:
                 raise TypeError("fused-optimizer aux_out must be the bf16 copy of the master weight")
         elif auxt.dtype != out.dtype:
@@ -347,19 +303,13 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
     L = _native.lib()
     in_dt = _native.dtype_code(a.dtype)
     out_dt = _native.dtype_code(torch.bfloat16 if out.dtype == torch.int16 else out.dtype)  # 16-bit planes
-    ksplit, ws, cnt = 1, None, None
+    ksplit, ws = 1, None
     if a.dtype == torch.bfloat16 and force in (None, "mfma_bf16"):
         ksplit = choose_ksplit(M, N, K)
         if ksplit > 1 and L.dllm_gemm_path(in_dt, out_dt, M, N, K, a.stride(0), b.stride(0), out.stride(0)) == 0:
             ws = _splitk_workspace(ksplit * M * N, a.device)
-            if _SEAM["enabled"]:
-                cnt = _splitk_counters((M // 256) * (N // 256) * 8, a.device)
         else:
             ksplit = 1
-    dws = None
-    if (epi == "sgd_split" and ksplit == 1 and _DEFER["enabled"] and K // 128 >= 17 and _POLICY["tpb"] > 1
-            and M % 256 == 0 and N % 256 == 0):
-        dws = _defer_workspace(defer_slab_floats(M, N), a.device)
     obs = _observe.active()
     if obs is not None:
         obs.gemm_begin()
@@ -372,10 +322,9 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
                      _native.stream_ptr(a.device), float(lr), float(betas[0]), float(betas[1]), float(eps),
                      float(wd), int(step), opt_m.data_ptr() if opt_m is not None else None,
                      opt_v.data_ptr() if opt_v is not None else None, ksplit,
-                     ws.data_ptr() if ws is not None else (dws.data_ptr() if dws is not None else None),
+                     ws.data_ptr() if ws is not None else None,
                      _mask_ptr(mask, M, N) if mask is not None else None,
-                     BF16_VARIANTS[_VARIANT["name"]], _POLICY["tpb"], _POLICY["min_bpc"],
-                     cnt.data_ptr() if cnt is not None else None, dws.numel() if dws is not None else 0)
+                     BF16_VARIANTS[_VARIANT["name"]], _POLICY["tpb"], _POLICY["min_bpc"])
     _native.check(rc, f"dllm_gemm({layout},{epi},M={M},N={N},K={K})")
     if obs is not None:
         obs.gemm_end()

@@ -43,7 +43,7 @@ import torch
 
 from ..models.ffn import (deinterleave_w13, interleave_w13, layer_bwd, layer_fwd, needs_preact,
                           recompute_fwd1)
-from ..ops.elementwise import adam_step_, cast_, sgd_split_step_, sgd_step_
+from ..ops.elementwise import adam_split_step_, adam_step_, cast_, sgd_split_step_, sgd_step_
 from ..ops.master import join_flat, part_flat, split_master
 from ..utils.config import TrainConfig
 from . import comm
@@ -226,8 +226,7 @@ class FFNTrainer:
         # bitwise the same fp32 values (ops/master.py).  4 B/param of weight state instead of 6 B, and every update
         # (fused wgrad epilogue or flat kernel) reads 4 B and writes 4 B per parameter instead of 4 B + 6 B.
         nmaster = self.shard_total if self.zero else self.total
-        self.split = (cfg.master == "split" and self.cd == torch.bfloat16 and cfg.optimizer == "sgd"
-                      and not self.side_opt)
+        self.split = cfg.master == "split" and self.cd == torch.bfloat16 and not self.side_opt
         if cfg.master not in ("split", "fp32"):
             raise ValueError(f"unknown master format {cfg.master!r}")
         self._master = None if self.split else torch.zeros(nmaster, dtype=torch.float32, device=dev)
@@ -639,11 +638,12 @@ class FFNTrainer:
     def _fused_wgrad_kw(self, l: int, name: str) -> dict:
         cfg = self.cfg
         if self.split:
-            return {"out": self._view(self.master_lo, self.entry[(l, name)]), "epi": "sgd_split", "lr": cfg.lr,
-                    "aux_out": self.copy_view(l, name)}
-        kw = {"out": self.master_view(l, name), "epi": cfg.optimizer, "lr": cfg.lr}
-        if not self.shared_copy:
-            kw["aux_out"] = self.copy_view(l, name)
+            kw = {"out": self._view(self.master_lo, self.entry[(l, name)]), "epi": cfg.optimizer + "_split",
+                  "lr": cfg.lr, "aux_out": self.copy_view(l, name)}
+        else:
+            kw = {"out": self.master_view(l, name), "epi": cfg.optimizer, "lr": cfg.lr}
+            if not self.shared_copy:
+                kw["aux_out"] = self.copy_view(l, name)
         if cfg.optimizer == "adam":
             e = self.entry[(l, name)]
             kw.update(betas=(cfg.adam_b1, cfg.adam_b2), eps=cfg.adam_eps, wd=cfg.weight_decay, step=self.step_count,
@@ -653,7 +653,12 @@ class FFNTrainer:
     def _opt(self, s: int, e: int) -> None:
         cfg = self.cfg
         if self.split:  # full or FSDP-shard layout: the residual plane shares the working copy's offsets
-            sgd_split_step_(self.master_lo[s:e], self.copy[s:e], self.grads[s:e], cfg.lr)
+            if cfg.optimizer == "sgd":
+                sgd_split_step_(self.master_lo[s:e], self.copy[s:e], self.grads[s:e], cfg.lr)
+            else:
+                adam_split_step_(self.master_lo[s:e], self.copy[s:e], self.grads[s:e], self.adam_m[s:e],
+                                 self.adam_v[s:e], self.step_count, cfg.lr, cfg.adam_b1, cfg.adam_b2, cfg.adam_eps,
+                                 cfg.weight_decay)
             return
         master, grad = self._master[s:e], self.grads[s:e]
         copy = None if self.shared_copy else self.copy[s:e]
@@ -725,8 +730,11 @@ class FFNTrainer:
         bf16_copy = self.cd == torch.bfloat16
         copy = self.copy[ss:se] if bf16_copy else None  # bf16: written by the optimizer kernel itself
         master = None if self.split else self._master[go:go + n]
-        if self.split:
+        if self.split and cfg.optimizer == "sgd":
             sgd_split_step_(self.master_lo[go:go + n], copy, g, cfg.lr)
+        elif self.split:
+            adam_split_step_(self.master_lo[go:go + n], copy, g, self.adam_m[go:go + n], self.adam_v[go:go + n],
+                             self.step_count, cfg.lr, cfg.adam_b1, cfg.adam_b2, cfg.adam_eps, cfg.weight_decay)
         elif cfg.optimizer == "sgd":
             sgd_step_(master, g, cfg.lr, copy=copy)
         else:

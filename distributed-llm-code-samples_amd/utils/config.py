@@ -85,7 +85,7 @@ class TrainConfig:
     comm_backend: str = "torch"      # torch (ProcessGroupNCCL/gloo) | native (csrc/comm.cpp RCCL layer)
     tp_allreduce: str = "rccl"       # TP activation all-reduce: rccl (role communicator) | custom (csrc/car.hip)
     debug_sync: bool = False         # race screen: wait every collective at issue + device sync per layer
-    master: str = "split"            # fp32 master weights of a bf16 SGD run: split (the bf16 working copy + an int16
+    master: str = "split"            # fp32 master weights of a bf16 run: split (the bf16 working copy + an int16
                                      # residual plane, together exactly the fp32 master: 4 B/param of weight state,
                                      # ops/master.py) | fp32 (a separate fp32 master next to the bf16 copy: 6 B/param)
     fp32_gemm: str = "bf16x6"        # fp32 compute GEMMs (process-wide): bf16x6 (exact 3-way bf16 split on the

@@ -29,7 +29,7 @@ def plan(D: int, F: int, L: int, tokens: int, dp: int = 1, tp: int = 1, mode: st
     """Per-rank bytes by buffer (and GiB totals).  ``mode``: none | ddp | zero | fsdp (over ``dp`` ranks).
     ``wgrad_stream``: the concurrent weight-gradient stream (single device, fused optimizer, kept activations, no
     TP) rotates two dgrad and three dx buffers instead of one and two (``FFNTrainer.da_ring`` / ``dxb``).
-    ``master``: "split" keeps a bf16 SGD run's fp32 master as the working copy plus an int16 residual plane
+    ``master``: "split" keeps a bf16 run's fp32 master as the working copy plus an int16 residual plane
     (``master_residual``, 2 B/param) instead of a separate fp32 buffer (``master_fp32``, 4 B/param)."""
     cd = 2 if dtype == "bf16" else 4
     gd = 2 if grad_dtype == "bf16" else 4
@@ -42,7 +42,7 @@ def plan(D: int, F: int, L: int, tokens: int, dp: int = 1, tp: int = 1, mode: st
     total = L * (_round_up(own(R1 * D), al) + _round_up(own(D * F_loc), al))
     master_n = total // dp if zero else total
     b = {}
-    if master == "split" and dtype == "bf16" and optimizer == "sgd":
+    if master == "split" and dtype == "bf16":
         b["master_residual"] = master_n * 2
     else:
         b["master_fp32"] = master_n * 4

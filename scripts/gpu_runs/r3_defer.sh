@@ -5,7 +5,7 @@ source scripts/gpu_steps.sh
 export TMPDIR=/tmp
 step pytest_defer 300 python -u -m pytest tests/test_defer_sgd_gpu.py -x -v --timeout 120 --timeout-method thread
 step pytest_seam 600 python -u -m pytest tests/test_gemm_gpu.py -x -q -k "splitk or seam or persistent or race" --timeout 200 --timeout-method thread
-step pytest_split 300 python -u -m pytest tests/test_split_master_gpu.py -x -q --timeout 120 --timeout-method thread
+step pytest_split 300 python -u -m pytest tests/test_split_master_gpu.py -x -v --timeout 120 --timeout-method thread
 for r in 1 2; do
   step head_defer_$r 300 python -u bench.py --methods none --steps 20 --warmup 5
   step head_nodefer_$r 300 python -u bench.py --methods none --steps 20 --warmup 5 --no_defer_sgd

@@ -497,82 +497,3 @@ def test_race_screen_repeated_runs_bitwise(layout, M, N, K, family):
     got = first[:256].cpu().double()
     assert ((got - ref).abs().max() / ref.abs().max()) < 1e-5
 
-
-@pytest.mark.parametrize("layout,epi", [("tn", "store_f32"), ("nt", "store"), ("nt", "act"), ("nn", "dact"),
-                                        ("tn", "sgd"), ("tn", "sgd_split"), ("tn", "adam"), ("nt", "glu")])
-def test_splitk_seam_matches_reduce_pass(layout, epi):
-    """Split-K slices combined inside the GEMM (last-arriving wave per (tile, wave) sums the sc1-published partials in
-    slice order) == the separate splitk_reduce pass, and bitwise run to run whatever the arrival order (5 repeats)."""
-    from dllm.ops.gemm import choose_ksplit, set_splitk, set_splitk_seam
-    from dllm.ops.master import split_master
-
-    M, N, K = 512, 768, 3072    # 6 tiles -> split 8 (slices per tile > 2: the summation order matters)
-    set_splitk(True)
-    assert choose_ksplit(M, N, K) > 2
-    a, b = _operands(layout, M, N, K, torch.bfloat16, seed=51)
-    a, b = a.cuda(), b.cuda()
-    w0 = _mk((M, N), torch.float32, 9).cuda() * 0.02
-
-    def run():
-        kw = {}
-        if epi == "store_f32":
-            out = torch.zeros(M, N, device="cuda")
-        elif epi in ("store", "act", "dact", "glu"):
-            out = torch.zeros(M, N // 2 if epi == "glu" else N, dtype=torch.bfloat16, device="cuda")
-            if epi == "act":
-                kw = dict(epi="act", act="gelu", aux_out=torch.zeros(M, N, dtype=torch.bfloat16, device="cuda"))
-            elif epi == "dact":
-                kw = dict(epi="dact", act="silu", aux=_mk((M, N), torch.bfloat16, 5).cuda())
-            elif epi == "glu":
-                kw = dict(epi="glu", act="silu", aux_out=torch.zeros(M, N, dtype=torch.bfloat16, device="cuda"))
-        elif epi == "sgd_split":
-            hi, out = split_master(w0)
-            kw = dict(epi="sgd_split", lr=1e-2, aux_out=hi)
-        else:
-            out = w0.clone()
-            kw = dict(epi=epi, lr=1e-2, aux_out=torch.zeros(M, N, dtype=torch.bfloat16, device="cuda"))
-            if epi == "adam":
-                kw.update(step=2, opt_m=torch.full((M, N), 0.01, device="cuda"),
-                          opt_v=torch.full((M, N), 1e-4, device="cuda"))
-        gemm(a, b, layout, out=out, **kw)
-        torch.cuda.synchronize()
-        return [out] + [v for v in kw.values() if isinstance(v, torch.Tensor)]
-
-    try:
-        set_splitk_seam(False)
-        ref = run()
-        set_splitk_seam(True)
-        outs = [run() for _ in range(5)]
-    finally:
-        set_splitk_seam(True)
-    for o in outs[1:]:
-        for x, y in zip(outs[0], o):
-            assert torch.equal(x, y)
-    for x, y in zip(outs[0], ref):
-        if x.dtype == torch.int16:
-            x, y = x.int(), y.int()
-            assert (x - y).abs().max() <= 1   # residual planes: the fp32 masters agree to the last bit or one ulp
-            continue
-        tol = 1e-2 if x.dtype == torch.bfloat16 else 1e-6
-        torch.testing.assert_close(x.float(), y.float(), rtol=tol, atol=tol * float(y.float().abs().max() + 1e-30))
-
-
-def test_splitk_seam_runs_no_reduce_kernel():
-    """The default split-K path is one launch: no splitk_reduce kernel in the trace."""
-    from torch.profiler import ProfilerActivity, profile
-
-    from dllm.ops.gemm import choose_ksplit, set_splitk
-
-    set_splitk(True)
-    M, N, K = 512, 512, 2048
-    assert choose_ksplit(M, N, K) > 1
-    a, b = _operands("tn", M, N, K, torch.bfloat16, seed=52)
-    a, b, out = a.cuda(), b.cuda(), torch.zeros(M, N, device="cuda")
-    gemm(a, b, "tn", out=out)
-    torch.cuda.synchronize()
-    with profile(activities=[ProfilerActivity.CUDA]) as prof:
-        gemm(a, b, "tn", out=out)
-        torch.cuda.synchronize()
-    names = [e.name for e in prof.events()]
-    assert any("gemm_bf16_8ph" in n for n in names), names
-    assert not any("splitk_reduce" in n for n in names), names

@@ -57,14 +57,17 @@ def test_engine_split_state_and_step():
     es, ef = _engine("split"), _engine("fp32")
     assert es.split and not ef.split and es.master_lo.dtype == torch.int16
     assert es.master_bytes * 2 == ef.master_bytes   # 2 B/param residual vs 4 B/param fp32
-    assert not _engine("split", opt="adam").split   # AdamW keeps an fp32 master
     layers = _layers(D, F, L)
     g = torch.Generator().manual_seed(3)
     x, dy = torch.randn(64, D, generator=g).bfloat16(), (torch.randn(64, D, generator=g) * 0.1).bfloat16()
-    for e in (es, ef):
+    ea, eb = _engine("split", opt="adam"), _engine("fp32", opt="adam")   # AdamW: split master, fp32 moments
+    assert ea.split and not eb.split
+    for e in (es, ef, ea, eb):
         e.load_full_params(layers)
         e.train_step(x, dy)
     assert torch.equal(es.master.view(torch.int32), ef.master.view(torch.int32))
+    assert torch.equal(ea.master.view(torch.int32), eb.master.view(torch.int32))
+    assert torch.equal(ea.adam_v, eb.adam_v)
     assert torch.equal(es.master_slice(3, 70), es.master[3:70])
     assert torch.equal(es.copy.view(torch.int16), split_master(es.master)[0].view(torch.int16))
 
@@ -87,8 +90,8 @@ def test_split_master_checkpoint_roundtrip(fmt, tmp_path):
             assert torch.equal(b.copy.view(torch.int16), a.copy.view(torch.int16))
 
 
-@pytest.mark.parametrize("method", [6, 2, 3])   # ZeRO-2, DDP, FSDP
-def test_split_master_data_parallel_equals_fp32(method, free_port):
+@pytest.mark.parametrize("method,opt", [(6, "sgd"), (2, "sgd"), (3, "sgd"), (6, "adam"), (3, "adam")])
+def test_split_master_data_parallel_equals_fp32(method, opt, free_port):
     """One step per rank over 2 gloo ranks from bf16-representable weights: the split-master engine's fp32 master equals the
     fp32-master engine's bit for bit (ZeRO-2 / DDP / FSDP shard updates run the flat split kernel)."""
     from dllm.parallel.launch import spawn
@@ -98,7 +101,7 @@ def test_split_master_data_parallel_equals_fp32(method, free_port):
     res = {}
     for i, fmt in enumerate(("split", "fp32")):
         cfg = TrainConfig(model=ModelConfig(D, F, L), batch_size=1, seq_len=64, num_steps=2, lr=1e-2, dtype="bf16",
-                          grad_dtype="bf16", data="cpu_compat", master=fmt)
+                          grad_dtype="bf16", data="cpu_compat", master=fmt, optimizer=opt)
         res[fmt] = spawn(2, cfg, method, "gloo", free_port + i,
                          {"seed": 11, "params": layers, "return_full": True, "tp": 2})["params"]
     for ps, pf in zip(res["split"], res["fp32"]):

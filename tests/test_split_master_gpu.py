@@ -99,3 +99,49 @@ def test_engine_split_master_step_equals_fp32(wgrad_stream):
         torch.cuda.synchronize()
         outs.append(eng.master.clone())
     assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
+
+
+@pytest.mark.parametrize("variant,tpb,shape", [("8phase_stagger", 8, (2048, 1536, 1024)), ("pp", 1, (2048, 1536, 1024)),
+                                               ("8phase_stagger", 8, (512, 512, 2048)), ("8phase_stagger", 8,
+                                                                                          (200, 136, 96))])
+def test_fused_adam_split_matches_fp32_master(variant, tpb, shape):
+    """AdamW on a split master (fused epilogue: 8-phase persistent, 256x128, split-K seam, generic) == AdamW on an fp32
+    master, to fp32 rounding of the moment math (the two epilogues may contract differently)."""
+    M, N, K = shape
+    old_v, old_t = set_bf16_variant(variant), set_tiles_per_block(tpb)
+    try:
+        a, b, w = _pair(M, N, K, 11)
+        kw = dict(lr=1e-3, betas=(0.9, 0.95), eps=1e-8, wd=0.01, step=3)
+        m0 = torch.full((M, N), 1e-3, device="cuda")
+        v0 = torch.full((M, N), 1e-6, device="cuda")
+        m32, ma, va = w.clone(), m0.clone(), v0.clone()
+        gemm(a, b, "tn", out=m32, epi="adam", aux_out=w.to(torch.bfloat16), opt_m=ma, opt_v=va, **kw)
+        hi, lo = split_master(w)
+        mb, vb = m0.clone(), v0.clone()
+        gemm(a, b, "tn", out=lo, epi="adam_split", aux_out=hi, opt_m=mb, opt_v=vb, **kw)
+        torch.cuda.synchronize()
+        torch.testing.assert_close(join_master(hi, lo), m32, rtol=1e-6, atol=1e-9)
+        torch.testing.assert_close(mb, ma, rtol=1e-6, atol=1e-12)
+        torch.testing.assert_close(vb, va, rtol=1e-6, atol=1e-15)
+    finally:
+        set_bf16_variant(old_v)
+        set_tiles_per_block(old_t)
+
+
+def test_flat_adam_split_kernel():
+    from dllm.ops.elementwise import adam_split_step_, adam_step_
+
+    g = torch.Generator().manual_seed(12)
+    n = 1 << 18
+    w = (torch.randn(n, generator=g) * 0.02).cuda()
+    grad = torch.randn(n, generator=g).to(torch.bfloat16).cuda()
+    ma, va = torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda")
+    m32 = w.clone()
+    adam_step_(m32, grad, ma, va, 1, 1e-3, wd=0.01)
+    hi = torch.empty(n, dtype=torch.bfloat16, device="cuda")
+    lo = torch.empty(n, dtype=torch.int16, device="cuda")
+    part_flat(w, hi, lo)
+    mb, vb = torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda")
+    adam_split_step_(lo, hi, grad, mb, vb, 1, 1e-3, wd=0.01)
+    torch.testing.assert_close(join_flat(hi, lo), m32, rtol=1e-6, atol=1e-9)
+    torch.testing.assert_close(vb, va, rtol=1e-6, atol=1e-15)
