@@ -19,7 +19,7 @@ def _train(side, fused, dtype="bf16"):
     layers = [init_ffn_layer(D, F, gen) for _ in range(L)]
     batches = list(reference_mock_data(torch.randint(100_000, (4,), generator=gen), T, D))
     cfg = TrainConfig(model=ModelConfig(D, F, L), batch_size=1, seq_len=T, dtype=dtype, grad_dtype=dtype,
-                      lr=1e-2, side_optimizer=side, fused_optimizer=fused)
+                      lr=1e-2, side_optimizer=side, fused_optimizer=fused, master="fp32")  # side opt: fp32 master
     dev = torch.device("cuda", 0)
     eng = FFNTrainer(cfg, Mesh.build(1, 1, device=dev), dev)
     assert eng.side_opt == (side > 0)
