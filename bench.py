@@ -129,9 +129,11 @@ def parse(argv=None):
     p.add_argument("--wgrad_stream", action=argparse.BooleanOptionalAction, default=True,
                    help="N=1 fused path: weight-gradient GEMMs (fused SGD) on a second stream, concurrent with the "
                         "dgrads; the dispatcher fills each GEMM's tail with the other's blocks (0.5 %% faster in 5/5 "
-                        "interleaved pairs, profiles/r2/wgrad_stream_ab_r2.log); --no-wgrad_stream = serial.  Not for "
-                        "gated (SwiGLU) stacks: there the serial step is 1.4 %% faster (167.0 vs 169.3 ms, "
-                        "profiles/r3/gated_wgrad_stream_q16_r3.txt)")
+                        "interleaved pairs, profiles/r2/wgrad_stream_ab_r2.log); --no-wgrad_stream = serial.  The "
+                        "engine uses it only while a weight gradient has <= 4 tiles per CU (TrainConfig."
+                        "wgrad_stream_max_tpc): D8192 (16 per CU) runs 131.5 ms concurrent vs 117.8 serial, the gated "
+                        "Llama dims (7 per CU) 169.3 vs 167.0 (profiles/r3/wgrad_stream_tiles_per_cu_r3.txt, "
+                        "gated_wgrad_stream_q16_r3.txt)")
     p.add_argument("--data_overlap", action="store_true",
                    help="one-deep data pipeline: draw the next step's batch on a side stream under the current "
                         "backward (default: each batch on the compute stream at the start of its step).  The draw "
@@ -212,7 +214,7 @@ def run_method(a, method: str, n: int, world: int, dev: torch.device, steps: int
                       side_optimizer=a.side_opt if headline else 0, tp_allreduce=a.tp_allreduce,
                       relu_mask=not a.no_relu_mask, gemm_tiles_per_block=a.tpb, fp32_gemm=a.fp32_gemm,
                       gemm_min_bpc=a.min_bpc, master=a.master,
-                      wgrad_stream=a.wgrad_stream and headline and not a.graph and not a.gated)
+                      wgrad_stream=a.wgrad_stream and headline and not a.graph)
     mesh = Mesh.build(dp, tp, force=force_comm, comm_backend="torch" if cpu else a.comm,
                       device=None if cpu else dev)
     try:

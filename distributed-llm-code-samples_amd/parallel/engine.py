@@ -315,9 +315,15 @@ class FFNTrainer:
         # chain (da, dx) stays on the compute stream, dW2 / dW1 run on a side stream after the dgrad that
         # last reads the weight they update; da / dx buffers rotate so the side stream's reads never race
         # the next layers' writes
+        # Only for weight gradients of at most `wgrad_stream_max_tpc` 256x256 tiles per CU: there the two streams'
+        # GEMMs fill each other's last tile wave (flagship D4096: 4 per CU, 0.4-1.1 % faster); with many tiles per CU
+        # nothing is left to fill and the two concurrent GEMMs only split L2 / MALL (D8192 F32768, 16 per CU: 131.5 vs
+        # 117.8 ms serial; profiles/r3/wgrad_stream_tiles_per_cu_r3.txt)
         self.wg_stream = None
+        wg_tiles = -(-self.R1 // 256) * -(-D // 256)
+        ncu = torch.cuda.get_device_properties(dev).multi_processor_count if dev.type == "cuda" else 256
         if (cfg.wgrad_stream and self.fused_opt and dev.type == "cuda" and not self.tp_comm and not self.sp
-                and cfg.recompute == "none"):
+                and cfg.recompute == "none" and wg_tiles <= cfg.wgrad_stream_max_tpc * ncu):
             self.wg_stream = torch.cuda.Stream(device=dev)
             self.da_ring = [self.da, torch.empty_like(self.da)]
             self.da_free = [None, None]

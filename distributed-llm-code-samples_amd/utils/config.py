@@ -71,6 +71,8 @@ class TrainConfig:
                                      # GEMM instead of the bf16 activation (GPU, 8-phase kernel shapes)
     wgrad_stream: bool = False       # single device, fused optimizer: weight-gradient GEMMs on a second
                                      # stream, concurrent with the dgrad chain (CUs shared; epilogues overlap)
+    wgrad_stream_max_tpc: float = 4.0  # wgrad_stream only while a weight gradient has <= this many 256x256 tiles
+                                     # per CU (larger ones run serially: concurrent big GEMMs only split L2 / MALL)
     gemm_min_bpc: int = 0            # persistent GEMM grids: minimum blocks per CU (0 = auto: 2 when collectives
                                      # overlap the GEMMs, else 1)
     gemm_tiles_per_block: int = 0    # persistent GEMM blocks (process-wide): cap on tiles per block; 0 = auto

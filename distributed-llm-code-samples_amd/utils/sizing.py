@@ -70,7 +70,9 @@ def plan(D: int, F: int, L: int, tokens: int, dp: int = 1, tp: int = 1, mode: st
         b["preactivations"] = nA * T * R1 * cd
     if relu_mask and act == "relu" and not gated and dtype == "bf16":
         b["relu_masks"] = nA * (T // 256) * (F_loc // 256) * 8192
-    ws = wgrad_stream and fused and tp == 1 and keep and not sp
+    # the engine runs the stream only while a weight gradient has <= 4 tiles per CU (TrainConfig.wgrad_stream_max_tpc)
+    ws = (wgrad_stream and fused and tp == 1 and keep and not sp
+          and -(-R1 // 256) * -(-D // 256) <= 4 * 256)
     b["dgrad_buffer"] = (2 if ws else 1) * T * R1 * cd
     b["dx_buffers"] = (3 if ws else 2) * T * D * cd
     if sp:
