@@ -146,6 +146,8 @@ def parse(argv=None):
     p.add_argument("--master", choices=["split", "fp32"], default="split",
                    help="fp32 master weights of a bf16 run: split (bf16 working copy + int16 residual, exactly the "
                         "fp32 master, 4 B/param) or a separate fp32 buffer (6 B/param with the copy)")
+    p.add_argument("--group_m_nt", type=int, default=4,
+                   help="tiles per raster band of the forward (NT) GEMMs (backward GEMMs: 4)")
     p.add_argument("--force_comm", action="store_true",
                    help="exercise the RCCL DDP/FSDP path of the headline at N=1 (size-1 communicators)")
     return p.parse_args(argv)
@@ -334,6 +336,10 @@ def main(argv=None) -> int:
         from dllm.ops.gemm import set_bf16_variant
 
         set_bf16_variant(a.gemm_variant)
+    if not cpu:
+        from dllm.ops.gemm import set_group_m_nt
+
+        set_group_m_nt(a.group_m_nt)
     ffn = a.ffn_dim or (a.mp_ffn_dim if a.method == "tp" else 0)
     model = ModelConfig(model_size=a.model_size, ffn_dim=ffn, layers=a.layers, act=a.act, gated=a.gated)
     head = run_method(a, a.method, n, world, dev, a.steps, a.warmup, a.force_comm, model,

@@ -227,7 +227,10 @@ _VARIANT = {"name": "auto"}
 # Launch policy of the 256x256 bf16 kernels (tiles per persistent block, minimum blocks per CU): Python-level
 # defaults that every call passes to the library explicitly -- the native side keeps no mutable state, so
 # GEMMs issued concurrently on different streams never race on a setting.
-_POLICY = {"tpb": 8, "min_bpc": 1}  # tpb: the cap; the library picks the makespan-optimal tiles per block
+# group_m_nt: tiles per raster band of the NT (forward) GEMMs.  8 is 1-1.3 % faster on the standalone forward shapes
+# (profiles/r3/group_m_sweep_r3.txt) but not in the step (30.15-30.37 vs 30.17-30.26 ms, interleaved,
+# profiles/r3/group_m_nt_step_r3.txt), so every layout keeps 4
+_POLICY = {"tpb": 8, "min_bpc": 1, "group_m_nt": 4}  # tpb: the cap; the library picks the makespan-optimal tiles per block
 # split-K fp32 partial workspaces, cached per (device, stream): a GEMM only ever reuses its own stream's
 # buffer, so stream order serialises the reuse
 _WS: dict = {}
@@ -244,7 +247,7 @@ def _splitk_workspace(numel: int, device: torch.device) -> torch.Tensor:
 
 def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None = None, *, epi: str = "store",
          act: str = "none", aux: torch.Tensor | None = None, aux_out: torch.Tensor | None = None,
-         alpha: float = 1.0, beta: float = 0.0, out_dtype: torch.dtype | None = None, group_m: int = 4,
+         alpha: float = 1.0, beta: float = 0.0, out_dtype: torch.dtype | None = None, group_m: int | None = None,
          force: str | None = None, lr: float = 0.0, betas: tuple = (0.9, 0.95), eps: float = 1e-8,
          wd: float = 0.0, step: int = 0, opt_m: torch.Tensor | None = None,
          opt_v: torch.Tensor | None = None, mask: torch.Tensor | None = None) -> torch.Tensor:
@@ -252,6 +255,8 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
     bitmask, ``epi="dact"`` reads it instead of ``aux`` (1 bit instead of a bf16 per element).  CPU tensors
     ignore it (``aux`` stays the source of truth there)."""
     M, N, K = gemm_shape(a, b, layout)
+    if group_m is None:   # raster band height: the layout's policy (profiles/r3/group_m_sweep_r3.txt)
+        group_m = _POLICY["group_m_nt"] if layout == "nt" else 4
     if a.dtype != b.dtype:
         raise TypeError(f"gemm operands differ in dtype: {a.dtype} vs {b.dtype}")
     nout = out_cols(N, epi)
@@ -371,6 +376,13 @@ def set_tiles_per_block(n: int) -> int:
     stack).  Returns the previous setting."""
     old = _POLICY["tpb"]
     _POLICY["tpb"] = max(1, int(n))
+    return old
+
+
+def set_group_m_nt(n: int) -> int:
+    """Tiles per raster band (L2 panel sharing) of the NT-layout GEMMs; returns the previous setting."""
+    old = _POLICY["group_m_nt"]
+    _POLICY["group_m_nt"] = max(1, int(n))
     return old
 
 
