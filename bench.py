@@ -134,6 +134,9 @@ def parse(argv=None):
                         "wgrad_stream_max_tpc): D8192 (16 per CU) runs 131.5 ms concurrent vs 117.8 serial, the gated "
                         "Llama dims (7 per CU) 169.3 vs 167.0 (profiles/r3/wgrad_stream_tiles_per_cu_r3.txt, "
                         "gated_wgrad_stream_q16_r3.txt)")
+    p.add_argument("--wgrad_stream_max_tpc", type=float, default=4.0,
+                   help="use the weight-gradient stream only while a weight gradient has at most this many 256x256 "
+                        "tiles per CU")
     p.add_argument("--data_overlap", action="store_true",
                    help="one-deep data pipeline: draw the next step's batch on a side stream under the current "
                         "backward (default: each batch on the compute stream at the start of its step).  The draw "
@@ -215,7 +218,7 @@ def run_method(a, method: str, n: int, world: int, dev: torch.device, steps: int
                       force_tp_comm=force_comm and method in ("tp", "hybrid"),
                       side_optimizer=a.side_opt if headline else 0, tp_allreduce=a.tp_allreduce,
                       relu_mask=not a.no_relu_mask, gemm_tiles_per_block=a.tpb, fp32_gemm=a.fp32_gemm,
-                      gemm_min_bpc=a.min_bpc, master=a.master,
+                      gemm_min_bpc=a.min_bpc, master=a.master, wgrad_stream_max_tpc=a.wgrad_stream_max_tpc,
                       wgrad_stream=a.wgrad_stream and headline and not a.graph)
     mesh = Mesh.build(dp, tp, force=force_comm, comm_backend="torch" if cpu else a.comm,
                       device=None if cpu else dev)
