@@ -365,12 +365,9 @@ class FFNTrainer:
     def master(self) -> torch.Tensor:
         """The fp32 master state this rank stores (full layout, FSDP row shards, or the ZeRO owned-shard layout).
 
-        fp32 format: the live buffer.  Split format: a materialised fp32 copy (joined from the bf16 working copy and
-        the int16 residual plane); writes to it take effect when ``refresh_copy`` runs (checkpoint load)."""
-        if not self.split:
-            return self._master
-        self._master_stage = self._join_master()
-        return self._master_stage
+        fp32 format: the live buffer.  Split format: a new fp32 tensor joined from the bf16 working copy and the int16
+        residual plane (read-only view of the state; writes go through ``flat_buffers`` + ``refresh_copy``)."""
+        return self._master if not self.split else self._join_master()
 
     @property
     def master_bytes(self) -> int:
@@ -515,6 +512,10 @@ class FFNTrainer:
         self.ddp_sync()
         self.fsdp_sync()
         out = {"params": self.master}
+        if self.split:
+            # a checkpoint load writes the fp32 master into this buffer; refresh_copy() splits it back (train_step
+            # drops it, so a stale one is never written over newer state)
+            self._master_stage = out["params"]
         if self.cfg.optimizer == "adam":
             out["adam_m"], out["adam_v"] = self.adam_m, self.adam_v
         return out
@@ -570,7 +571,7 @@ class FFNTrainer:
             self.fsdp_sync()
             self.ag_next.clear()  # gathered rings hold the old weights
         if self.split:
-            # the fp32 master was written through the buffer `master` last materialised (flat_buffers)
+            # the fp32 master was written through the buffer flat_buffers() handed out (checkpoint load)
             if self._master_stage is not None:
                 self._store_master(self._master_stage)
                 self._master_stage = None
@@ -883,6 +884,7 @@ class FFNTrainer:
         """
         cfg = self.cfg
         L, act, gated = self.L, self.act, self.gated
+        self._master_stage = None   # a checkpoint buffer handed out before this step is stale from here on
         self.step_count += 1
         keep = cfg.recompute == "none"
         tpg = self.mesh.group("tp")

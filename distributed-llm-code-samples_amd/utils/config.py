@@ -149,5 +149,8 @@ def add_extended_args(p: argparse.ArgumentParser) -> None:
     p.add_argument("--master_port", type=int, default=29500)
     p.add_argument("--fp32_gemm", choices=["bf16x6", "mfma_f32"], default="bf16x6",
                    help="how --dtype fp32 GEMMs run: exact bf16 3-way split on the bf16 matrix cores, or fp32 MFMA")
+    p.add_argument("--master", choices=["split", "fp32"], default="split",
+                   help="fp32 master weights of a bf16 run: split (bf16 working copy + int16 residual, bit-exact, "
+                        "4 B/param) or a separate fp32 buffer")
     p.add_argument("--debug_sync", action="store_true",
                    help="race screen: serialize every collective (must match the overlapped run bitwise)")
