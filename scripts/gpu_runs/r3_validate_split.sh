@@ -5,7 +5,7 @@ source scripts/gpu_steps.sh
 export TMPDIR=/tmp
 step pytest_gpu 1100 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step bench_default 600 python -u bench.py
+step bench_default 600 python -u bench.py --gpus 1 --steps 20 --warmup 5
 step head_split 300 python -u bench.py --methods none --steps 20 --warmup 5
 step head_fp32 300 python -u bench.py --methods none --steps 20 --warmup 5 --master fp32
 step head_trace 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_head -o head -- python bench.py --methods none --steps 10 --warmup 3
