@@ -151,6 +151,8 @@ def parse(argv=None):
                         "fp32 master, 4 B/param) or a separate fp32 buffer (6 B/param with the copy)")
     p.add_argument("--group_m_nt", type=int, default=4,
                    help="tiles per raster band of the forward (NT) GEMMs (backward GEMMs: 4)")
+    p.add_argument("--dist_first", action="store_true",
+                   help="diagnostic: create the process group before the N=1 headline (as N>1 runs must)")
     p.add_argument("--force_comm", action="store_true",
                    help="exercise the RCCL DDP/FSDP path of the headline at N=1 (size-1 communicators)")
     return p.parse_args(argv)
@@ -330,10 +332,16 @@ def main(argv=None) -> int:
     methods = [m for m in a.methods.split(",") if m and m != "none"]
     if not cpu:
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count()))
-    if world > 1 or a.force_comm or methods:
+    def init_dist():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
         init_distributed("gloo" if a.backend == "gloo_gpu" else a.backend)
+
+    # At N=1 the headline needs no process group: the side methods' one is created after it.  An RCCL communicator
+    # that exists while the headline runs costs it 1.3-2.2 % (30.54-30.70 vs 30.04-30.14 ms interleaved,
+    # profiles/r3/headline_rccl_init_order_r3.txt)
+    if world > 1 or a.force_comm or a.dist_first:
+        init_dist()
     dev = torch.device("cpu") if cpu else torch.device("cuda", torch.cuda.current_device())
     if a.gemm_variant != "auto" and not cpu:
         from dllm.ops.gemm import set_bf16_variant
@@ -347,6 +355,8 @@ def main(argv=None) -> int:
     model = ModelConfig(model_size=a.model_size, ffn_dim=ffn, layers=a.layers, act=a.act, gated=a.gated)
     head = run_method(a, a.method, n, world, dev, a.steps, a.warmup, a.force_comm, model,
                       observe_steps=a.observe_steps, headline=True)
+    if methods and not (world > 1 or a.force_comm or a.dist_first):
+        init_dist()
 
     side: dict = {}
 

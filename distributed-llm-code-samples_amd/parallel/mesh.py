@@ -46,7 +46,9 @@ def init_distributed(backend: str, rank: int | None = None, world_size: int | No
     if backend == "nccl":
         local = int(os.environ.get("LOCAL_RANK", rank))
         torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
-        kw["device_id"] = torch.device("cuda", torch.cuda.current_device())
+        # eager communicator creation (device_id) unless DLLM_NCCL_EAGER=0: then RCCL builds it at the first collective
+        if os.environ.get("DLLM_NCCL_EAGER", "1") != "0":
+            kw["device_id"] = torch.device("cuda", torch.cuda.current_device())
     dist.init_process_group(backend, rank=rank, world_size=world_size,
                             timeout=datetime.timedelta(seconds=timeout_s), **kw)
     return rank, world_size
