@@ -342,6 +342,14 @@ def main(argv=None) -> int:
     # profiles/r3/headline_rccl_init_order_r3.txt)
     if world > 1 or a.force_comm or a.dist_first:
         init_dist()
+    diag_streams = []
+    if os.environ.get("DLLM_DIAG_STREAMS") and not cpu:   # diagnostic: idle extra streams (count, priority)
+        cnt, _, prio = os.environ["DLLM_DIAG_STREAMS"].partition(":")
+        diag_streams = [torch.cuda.Stream(priority=int(prio or 0)) for _ in range(int(cnt))]
+        for st in diag_streams:   # touch each so its HW queue is live
+            with torch.cuda.stream(st):
+                torch.zeros(1, device="cuda").add_(1)
+        torch.cuda.synchronize()
     dev = torch.device("cpu") if cpu else torch.device("cuda", torch.cuda.current_device())
     if a.gemm_variant != "auto" and not cpu:
         from dllm.ops.gemm import set_bf16_variant
