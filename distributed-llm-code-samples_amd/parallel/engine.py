@@ -13,7 +13,8 @@ The reference has four separate workers (train_ffns.py:101-116 single, :156-193 
 MI355X-first memory design (288 GB HBM per GPU):
 
 * **Flat buffers in completion order.**  Every rank owns one flat fp32 master buffer (plus its bf16
-  compute copy, its gradient buffer and optional Adam moments) holding, for ``l = L-1 … 0``, the
+  compute copy, its gradient buffer and optional Adam moments; a bf16 run stores the fp32 master split, as the
+  compute copy plus an int16 residual plane, ``ops/master.py``) holding, for ``l = L-1 … 0``, the
   layer's ``W2`` then ``W1`` (= the order the backward finishes them).  Any contiguous range is
   therefore a valid gradient bucket that becomes ready all at once — DDP buckets are plain views,
   collectives are zero-copy, and the optimizer runs over ranges with one fused kernel.
