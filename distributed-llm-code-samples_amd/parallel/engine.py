@@ -46,6 +46,7 @@ from ..models.ffn import (deinterleave_w13, interleave_w13, layer_bwd, layer_fwd
                           recompute_fwd1)
 from ..ops.elementwise import adam_split_step_, adam_step_, cast_, sgd_split_step_, sgd_step_
 from ..ops.master import join_flat, part_flat, split_master
+from ..utils import streams
 from ..utils.config import TrainConfig
 from . import comm
 from .mesh import Mesh
@@ -238,7 +239,7 @@ class FFNTrainer:
         self.fused_opt = cfg.fused_optimizer and no_coll and not self.side_opt
         self.grads = torch.zeros(0 if self.fused_opt else self.total, dtype=self.gd, device=dev)
         if self.side_opt:
-            self.opt_stream_side = torch.cuda.Stream(device=dev)
+            self.opt_stream_side = self._side_stream("side_opt")
             self.opt_done = {}
         if cfg.optimizer == "adam":
             self.adam_m = torch.zeros(nmaster, dtype=torch.float32, device=dev)
@@ -254,7 +255,7 @@ class FFNTrainer:
             self.ag_layer = [-1, -1]
             self.rs_pending = [None, None]  # per slot: (layer, {name: work}) -- one reduce-scatter per weight
             self.ag_next = set()            # layers whose post-update gather for the next forward is in flight
-            self.fsdp_stream = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
+            self.fsdp_stream = self._side_stream("fsdp")
             self.fsdp_tail_ev = None
             self.fsdp_upd = {}              # layer -> event: its shard update on the side stream (backward)
 
@@ -325,7 +326,7 @@ class FFNTrainer:
         ncu = torch.cuda.get_device_properties(dev).multi_processor_count if dev.type == "cuda" else 256
         if (cfg.wgrad_stream and self.fused_opt and dev.type == "cuda" and not self.tp_comm and not self.sp
                 and cfg.recompute == "none" and wg_tiles <= cfg.wgrad_stream_max_tpc * ncu):
-            self.wg_stream = torch.cuda.Stream(device=dev)
+            self.wg_stream = self._side_stream("wgrad")
             self.da_ring = [self.da, torch.empty_like(self.da)]
             self.da_free = [None, None]
             self.dx_free = [None, None, None]
@@ -348,7 +349,7 @@ class FFNTrainer:
                                    for l in range(L) for n in ("w1", "w2")}
             # the step-boundary buckets' optimizer (+ ZeRO all-gather) run on a side stream so the next
             # step's first GEMM does not queue behind the last collective; the forward waits per weight
-            self.opt_stream = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
+            self.opt_stream = self._side_stream("opt")
             self.ddp_done = [None] * len(self.buckets)
         if self.zero:
             self.gshard = torch.zeros(self.shard_total, dtype=self.gd, device=dev)
@@ -873,6 +874,10 @@ class FFNTrainer:
         """Make the current stream wait for the step-boundary updates / gathers (checkpoint, readout)."""
         if self.fsdp and self.fsdp_stream is not None:
             torch.cuda.current_stream(self.device).wait_stream(self.fsdp_stream)
+
+    def _side_stream(self, role: str):
+        """The engine's stream for side-work ``role`` (utils/streams.py picks its hardware queue); None off the GPU."""
+        return streams.side_stream(self.device, role) if self.device.type == "cuda" else None
 
     # ------------------------------------------------------------------------------------------------
     # one training step

@@ -1,0 +1,53 @@
+"""Where the engine's side streams (weight-gradient, shard-optimizer, FSDP tail) get their hardware queues.
+
+HIP gives a process at most ``GPU_MAX_HW_QUEUES`` hardware queues per priority level; once they are taken it puts
+each new stream on the least-used existing queue, picked in pointer order.  torch's stream pool (32 streams, created
+together at its first use) and RCCL's internal streams take them early in a job with a process group, so a side
+stream can land on the compute stream's queue and the two streams' kernels serialise
+(``profiles/r3/hw_queue_collision_trace_r3.txt``: the weight-gradient stream lost all of its overlap that way).
+
+``DLLM_SIDE_STREAMS`` picks the remedy:
+  * ``pool`` (default): torch pool streams, as before;
+  * ``high``: native non-blocking streams at high priority (``csrc/comm.cpp: dllm_stream_create``).  HIP keeps a
+    separate queue set per priority, and nothing else in the process asks for high-priority queues, so these
+    never share the compute stream's (normal-priority) queue.
+
+More hardware queues are not the remedy: at 32 the hardware scheduler time-slices them and the communicating
+methods collapse (``profiles/r3/hw_queues_32_vs_16_r3.txt``); queues that own a CU mask cost 2 % on the headline
+(``profiles/r3/dedicated_cu_mask_queues_r3.txt``).  Native handles live for the process.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+from .. import _native
+
+_native.register_optional("dllm_stream_create", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)])
+_HANDLES: dict[tuple[int, str], torch.cuda.ExternalStream] = {}
+
+
+def mode() -> str:
+    m = os.environ.get("DLLM_SIDE_STREAMS", "pool")
+    if m not in ("pool", "high"):
+        raise ValueError(f"DLLM_SIDE_STREAMS={m!r}: expected pool | high")
+    return m
+
+
+def side_stream(device: torch.device, role: str) -> torch.cuda.Stream:
+    """The stream for side-work ``role`` on ``device`` (one per role and device under ``high``)."""
+    if mode() == "pool":
+        return torch.cuda.Stream(device=device)
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    key = (idx, role)
+    if key not in _HANDLES:
+        lo, hi = torch.cuda.Stream.priority_range() if hasattr(torch.cuda.Stream, "priority_range") else (0, -1)
+        h = ctypes.c_void_p()
+        with torch.cuda.device(idx):
+            rc = _native.lib().dllm_stream_create(int(hi), ctypes.byref(h))
+        if rc != 0 or not h.value:
+            raise RuntimeError(f"hipStreamCreateWithPriority failed ({rc})")
+        _HANDLES[key] = torch.cuda.ExternalStream(h.value, device=torch.device("cuda", idx))
+    return _HANDLES[key]
