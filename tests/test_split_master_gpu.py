@@ -145,3 +145,32 @@ def test_flat_adam_split_kernel():
     adam_split_step_(lo, hi, grad, mb, vb, 1, 1e-3, wd=0.01)
     torch.testing.assert_close(join_flat(hi, lo), m32, rtol=1e-6, atol=1e-9)
     torch.testing.assert_close(vb, va, rtol=1e-6, atol=1e-15)
+
+
+def test_engine_high_priority_side_streams_bitwise(monkeypatch):
+    """DLLM_SIDE_STREAMS=high (native high-priority wgrad / opt streams, utils/streams.py) changes only where the
+    side work is queued: the step's master is bitwise the pool-stream step's."""
+    from dllm.parallel.engine import FFNTrainer
+    from dllm.parallel.mesh import Mesh
+    from dllm.utils.config import ModelConfig, TrainConfig
+    from dllm.utils.data import DeviceMockData
+
+    D, F, L = 512, 2048, 3
+    g = torch.Generator().manual_seed(13)
+    layers = [{"w1": torch.randn(F, D, generator=g) * 0.02, "w2": torch.randn(D, F, generator=g) * 0.02}
+              for _ in range(L)]
+    outs = []
+    for mode in ("pool", "high"):
+        monkeypatch.setenv("DLLM_SIDE_STREAMS", mode)
+        cfg = TrainConfig(model=ModelConfig(D, F, L), batch_size=2, seq_len=512, dtype="bf16", grad_dtype="bf16",
+                          lr=1e-2, wgrad_stream=True)
+        eng = FFNTrainer(cfg, Mesh(), torch.device("cuda"))
+        assert eng.wg_stream is not None
+        assert isinstance(eng.wg_stream, torch.cuda.ExternalStream) == (mode == "high")
+        eng.load_full_params(layers)
+        x, dy = DeviceMockData(cfg.tokens, D, torch.bfloat16, torch.device("cuda")).fill(3)
+        for _ in range(2):
+            eng.train_step(x, dy)
+        torch.cuda.synchronize()
+        outs.append(eng.master.clone())
+    assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
