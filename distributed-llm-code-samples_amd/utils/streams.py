@@ -7,10 +7,14 @@ stream can land on the compute stream's queue and the two streams' kernels seria
 (``profiles/r3/hw_queue_collision_trace_r3.txt``: the weight-gradient stream lost all of its overlap that way).
 
 ``DLLM_SIDE_STREAMS`` picks the remedy:
-  * ``pool`` (default): torch pool streams, as before;
+  * ``pool`` (default): torch pool streams;
   * ``high``: native non-blocking streams at high priority (``csrc/comm.cpp: dllm_stream_create``).  HIP keeps a
     separate queue set per priority, and nothing else in the process asks for high-priority queues, so these
-    never share the compute stream's (normal-priority) queue.
+    never share the compute stream's (normal-priority) queue;
+  * ``auto``: ``high`` for the weight-gradient stream only (it runs only in steps without collectives).  It recovers
+    a step next to a live communicator (29.86-29.96 vs 30.32-30.43 ms) and is neutral without one, but collective
+    methods run later in the same process lose 5-14 % (``profiles/r3/side_streams_auto_r3.txt``); ``high`` costs
+    them about as much (DDP +6 %, hybrid +10 %, ``side_streams_high_priority_r3.txt``).  Hence not the default.
 
 More hardware queues are not the remedy: at 32 the hardware scheduler time-slices them and the communicating
 methods collapse (``profiles/r3/hw_queues_32_vs_16_r3.txt``); queues that own a CU mask cost 2 % on the headline
@@ -29,16 +33,24 @@ _native.register_optional("dllm_stream_create", ctypes.c_int, [ctypes.c_int, cty
 _HANDLES: dict[tuple[int, str], torch.cuda.ExternalStream] = {}
 
 
+HIGH_ROLES_AUTO = ("wgrad",)
+
+
 def mode() -> str:
     m = os.environ.get("DLLM_SIDE_STREAMS", "pool")
-    if m not in ("pool", "high"):
-        raise ValueError(f"DLLM_SIDE_STREAMS={m!r}: expected pool | high")
+    if m not in ("pool", "high", "auto"):
+        raise ValueError(f"DLLM_SIDE_STREAMS={m!r}: expected pool | high | auto")
     return m
 
 
+def high_priority(role: str) -> bool:
+    m = mode()
+    return m == "high" or (m == "auto" and role in HIGH_ROLES_AUTO)
+
+
 def side_stream(device: torch.device, role: str) -> torch.cuda.Stream:
-    """The stream for side-work ``role`` on ``device`` (one per role and device under ``high``)."""
-    if mode() == "pool":
+    """The stream for side-work ``role`` on ``device`` (one native stream per role and device at high priority)."""
+    if not high_priority(role):
         return torch.cuda.Stream(device=device)
     idx = device.index if device.index is not None else torch.cuda.current_device()
     key = (idx, role)

@@ -7,9 +7,11 @@ from dllm.utils import streams
 
 def test_mode_default_and_validation(monkeypatch):
     monkeypatch.delenv("DLLM_SIDE_STREAMS", raising=False)
-    assert streams.mode() == "pool"
+    assert streams.mode() == "pool" and not streams.high_priority("wgrad")
+    monkeypatch.setenv("DLLM_SIDE_STREAMS", "auto")
+    assert streams.high_priority("wgrad") and not streams.high_priority("opt") and not streams.high_priority("fsdp")
     monkeypatch.setenv("DLLM_SIDE_STREAMS", "high")
-    assert streams.mode() == "high"
+    assert streams.mode() == "high" and streams.high_priority("opt")
     monkeypatch.setenv("DLLM_SIDE_STREAMS", "masked")
     with pytest.raises(ValueError):
         streams.mode()
