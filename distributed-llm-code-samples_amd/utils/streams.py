@@ -14,7 +14,8 @@ stream can land on the compute stream's queue and the two streams' kernels seria
   * ``auto``: ``high`` for the weight-gradient stream only (it runs only in steps without collectives).  It recovers
     a step next to a live communicator (29.86-29.96 vs 30.32-30.43 ms) and is neutral without one, but collective
     methods run later in the same process lose 5-14 % (``profiles/r3/side_streams_auto_r3.txt``); ``high`` costs
-    them about as much (DDP +6 %, hybrid +10 %, ``side_streams_high_priority_r3.txt``).  Hence not the default.
+    them about as much (DDP +6 %, hybrid +10 %, ``side_streams_high_priority_r3.txt``).  A high-priority queue that
+    exists is enough for that loss; why is not pinned down.  Hence not the default.
 
 More hardware queues are not the remedy: at 32 the hardware scheduler time-slices them and the communicating
 methods collapse (``profiles/r3/hw_queues_32_vs_16_r3.txt``); queues that own a CU mask cost 2 % on the headline
