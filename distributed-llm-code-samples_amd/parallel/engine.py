@@ -877,7 +877,7 @@ class FFNTrainer:
 
     def _side_stream(self, role: str):
         """The engine's stream for side-work ``role`` (utils/streams.py picks its hardware queue); None off the GPU."""
-        return streams.side_stream(self.device, role) if self.device.type == "cuda" else None
+        return streams.side_stream(self.device, role, owner=self) if self.device.type == "cuda" else None
 
     # ------------------------------------------------------------------------------------------------
     # one training step

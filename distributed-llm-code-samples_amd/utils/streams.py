@@ -25,12 +25,14 @@ from __future__ import annotations
 
 import ctypes
 import os
+import weakref
 
 import torch
 
 from .. import _native
 
 _native.register_optional("dllm_stream_create", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)])
+_native.register_optional("dllm_stream_destroy", ctypes.c_int, [ctypes.c_void_p])
 _HANDLES: dict[tuple[int, str], torch.cuda.ExternalStream] = {}
 
 
@@ -49,18 +51,32 @@ def high_priority(role: str) -> bool:
     return m == "high" or (m == "auto" and role in HIGH_ROLES_AUTO)
 
 
-def side_stream(device: torch.device, role: str) -> torch.cuda.Stream:
-    """The stream for side-work ``role`` on ``device`` (one native stream per role and device at high priority)."""
+def _destroy(handle: int, idx: int) -> None:
+    try:
+        torch.cuda.synchronize(idx)
+        _native.lib().dllm_stream_destroy(handle)
+    except Exception:
+        pass
+
+
+def side_stream(device: torch.device, role: str, owner=None) -> torch.cuda.Stream:
+    """The stream for side-work ``role`` on ``device``.  A high-priority one is native; with ``owner`` it is destroyed
+    (its hardware queue released) when the owner is collected, else it is cached for the process."""
     if not high_priority(role):
         return torch.cuda.Stream(device=device)
     idx = device.index if device.index is not None else torch.cuda.current_device()
     key = (idx, role)
-    if key not in _HANDLES:
-        lo, hi = torch.cuda.Stream.priority_range() if hasattr(torch.cuda.Stream, "priority_range") else (0, -1)
-        h = ctypes.c_void_p()
-        with torch.cuda.device(idx):
-            rc = _native.lib().dllm_stream_create(int(hi), ctypes.byref(h))
-        if rc != 0 or not h.value:
-            raise RuntimeError(f"hipStreamCreateWithPriority failed ({rc})")
-        _HANDLES[key] = torch.cuda.ExternalStream(h.value, device=torch.device("cuda", idx))
-    return _HANDLES[key]
+    if owner is None and key in _HANDLES:
+        return _HANDLES[key]
+    lo, hi = torch.cuda.Stream.priority_range() if hasattr(torch.cuda.Stream, "priority_range") else (0, -1)
+    h = ctypes.c_void_p()
+    with torch.cuda.device(idx):
+        rc = _native.lib().dllm_stream_create(int(hi), ctypes.byref(h))
+    if rc != 0 or not h.value:
+        raise RuntimeError(f"hipStreamCreateWithPriority failed ({rc})")
+    st = torch.cuda.ExternalStream(h.value, device=torch.device("cuda", idx))
+    if owner is None:
+        _HANDLES[key] = st
+    else:
+        weakref.finalize(owner, _destroy, h.value, idx)
+    return st
