@@ -5,8 +5,13 @@ MI355X" on the 8-layer hidden=4096 FFN stack (FFN = 4·hidden = 16384, ReLU, as 
 batch 8 × seq 1024 = 8192 tokens per rank per step, bf16 compute with fp32 master weights, SGD (the
 reference optimizer, train_ffns.py:172), random-init weights and synthetic device-generated data.
 
-    python bench.py --gpus N --steps K --warmup W            # N=1 in-process
+    python bench.py --gpus N --steps K --warmup W            # N=1 in-process; N>1: starts its own N ranks
     torchrun --nproc-per-node N bench.py --gpus N ...          # one rank per GPU over RCCL/xGMI
+
+With N > 1 and no launcher environment (no ``WORLD_SIZE``), the process launches its own N ranks the way the
+reference's ``train_ffns.py`` does (one worker per GPU from a plain ``python`` command, train_ffns.py:184-191,
+:375): fresh child interpreters with ``RANK``/``LOCAL_RANK``/``WORLD_SIZE``/``MASTER_*`` set, started before this
+process imports torch (so it never touches HIP), rank 0's stdout relayed, any failing rank failing the run.
 
 Each timed step is the full training step: device mock-data generation, forward, backward (all weight
 and input gradients except the unused layer-0 input grad), gradient communication and the optimizer
@@ -42,19 +47,72 @@ import argparse
 import gc
 import json
 import os
+import signal
+import socket
+import subprocess
 import sys
 import threading
 import time
 
-import torch
 
-import dllm  # noqa: F401
-from dllm.parallel import comm
-from dllm.parallel.engine import FFNTrainer
-from dllm.parallel.mesh import Mesh, init_distributed
-from dllm.utils.config import ModelConfig, TrainConfig
-from dllm.utils.data import DeviceMockData
-from dllm.utils.metrics import flops_per_step, peak_tflops
+def _requested_ranks(argv) -> int:
+    p = argparse.ArgumentParser(add_help=False)
+    p.add_argument("--gpus", type=int, default=0)
+    return p.parse_known_args(argv)[0].gpus
+
+
+def self_launch(argv, n: int, grace_s: float = 30.0) -> int:
+    """Start ``n`` ranks of this script as child interpreters (stdlib only: no torch / HIP in this process) and
+    wait for them.  Rank 0 keeps this process's stdout (the one JSON line); the other ranks' stdout goes to stderr.
+    The first rank that fails ends the others after ``grace_s`` (they may be blocked in a collective with it);
+    the exit code is the first non-zero rank exit code, or 0.  SIGTERM/SIGINT are forwarded to every rank."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DLLM_SELF_LAUNCHED="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env,
+                                      stdout=None if r == 0 else sys.stderr))
+
+    def forward(sig, _frame):
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(sig)
+
+    signal.signal(signal.SIGTERM, forward)
+    signal.signal(signal.SIGINT, forward)
+    rc, failed_at = 0, None
+    while any(p.poll() is None for p in procs):
+        for r, p in enumerate(procs):
+            if p.returncode not in (None, 0) and rc == 0:
+                rc, failed_at = p.returncode, time.monotonic()
+                print(f"bench.py: rank {r} exited with {p.returncode}", file=sys.stderr, flush=True)
+        if failed_at is not None and time.monotonic() - failed_at > grace_s:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+        time.sleep(0.2)
+    for r, p in enumerate(procs):
+        if p.returncode != 0 and rc == 0:
+            rc = p.returncode
+            print(f"bench.py: rank {r} exited with {p.returncode}", file=sys.stderr, flush=True)
+    return rc if rc >= 0 else 128 - rc  # a rank killed by signal k -> 128 + k
+
+
+if __name__ == "__main__" and "WORLD_SIZE" not in os.environ and _requested_ranks(sys.argv[1:]) > 1:
+    sys.exit(self_launch(sys.argv[1:], _requested_ranks(sys.argv[1:])))
+
+import torch  # noqa: E402
+
+import dllm  # noqa: F401,E402
+from dllm.parallel import comm  # noqa: E402
+from dllm.parallel.engine import FFNTrainer  # noqa: E402
+from dllm.parallel.mesh import Mesh, init_distributed  # noqa: E402
+from dllm.utils.config import ModelConfig, TrainConfig  # noqa: E402
+from dllm.utils.data import DeviceMockData  # noqa: E402
+from dllm.utils.metrics import flops_per_step, peak_tflops  # noqa: E402
 
 METRIC = "FFN tokens/sec (whole node) at hidden=4096 for DDP/FSDP/MP, 1/2/4/8 MI355X"
 MP_FFN = 14336  # BASELINE.json config 4: FFN (hidden=4096, ffn=14336) MP column/row split
@@ -295,7 +353,9 @@ def _run_on_mesh(a, method, cfg, mesh, n, world, dev, steps, warmup, force_comm,
            "master": "fp32 (split: bf16 working copy + int16 residual)" if eng.split else "fp32",
            "global_batch": a.batch_size * dp, "parallelism": parallelism(method, n, dp, tp, world, force_comm),
            "model": model_name(model), "steps": steps, "warmup": warmup, "state_gib": state_gib(eng),
-           "wgrad_stream": eng.wg_stream is not None}
+           "wgrad_stream": eng.wg_stream is not None,
+           # the ranks each role communicator actually spans (RCCL / gloo group sizes; {} = no collective)
+           "comm_sizes": {role: g.size() for role, g in mesh.groups.items() if g is not None}}
     if phases:
         rec["phase_ms_per_step"] = phases
     communicates = bool(mesh.groups) or eng.tp_car is not None
@@ -327,7 +387,7 @@ def main(argv=None) -> int:
     rank = int(os.environ.get("RANK", "0"))
     n = a.gpus or world
     if n != world:
-        raise SystemExit(f"--gpus {n} but WORLD_SIZE={world}: launch N>1 with torchrun")
+        raise SystemExit(f"--gpus {n} but WORLD_SIZE={world}: the launcher started a different number of ranks")
     cpu = a.backend == "gloo"
     methods = [m for m in a.methods.split(",") if m and m != "none"]
     if not cpu:
@@ -367,10 +427,14 @@ def main(argv=None) -> int:
         init_dist()
 
     side: dict = {}
+    import torch.distributed as dist
 
     def record(note: str = "") -> dict:
         rec = {
-            "metric": METRIC, "value": head["value"], "unit": "tokens/s", "n_gpus": 0 if cpu else n,
+            "metric": METRIC, "value": head["value"], "unit": "tokens/s", "n_gpus": n,
+            "world_size": dist.get_world_size() if dist.is_initialized() else 1, "comm_sizes": head["comm_sizes"],
+            "launcher": "self" if os.environ.get("DLLM_SELF_LAUNCHED") else ("torchrun" if world > 1 else "none"),
+            "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "default"),
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": head["ms_per_step"], "higher_is_better": True,
             "scaling": "strong" if a.method == "tp" else "weak", "vs_baseline": None, "dtype": a.dtype,
             "data": "synthetic (device Philox N(0,1) x, 0.1*N(0,1) dloss/dx, drawn every step" +
@@ -461,8 +525,6 @@ def main(argv=None) -> int:
         side[m] = {k: r[k] for k in SIDE_KEYS if k in r}
     current["m"] = None
     emit(record())
-    import torch.distributed as dist
-
     if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()

@@ -8,6 +8,15 @@
 
 using namespace dllm;
 
+// --gemm_variant pp workgroup-slot skew (experiment knob): read once when the library loads, not per launch
+static int pp_skew() {
+  static const int skew = [] {
+    const char* sk = getenv("DLLM_PP_SKEW");
+    return sk ? atoi(sk) : 0;
+  }();
+  return skew;
+}
+
 extern "C" {
 
 // Returns 0 on success, a hipError_t otherwise, or -1 for a bad argument.
@@ -34,10 +43,7 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
   a.tpb_req = tpb;
   a.min_bpc = min_bpc < 1 ? 1 : min_bpc;
   a.ws = nullptr;
-  {
-    const char* sk = getenv("DLLM_PP_SKEW");
-    a.skew = sk ? atoi(sk) : 0;
-  }
+  a.skew = pp_skew();
   // the LDS-DMA loads and 16-B / paired epilogue accesses of the MFMA paths need 16-B aligned bases
   const bool aligned_ptr = ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && ((uintptr_t)C % 16 == 0) &&
                            ((uintptr_t)aux % 16 == 0) && ((uintptr_t)aux_out % 16 == 0) &&

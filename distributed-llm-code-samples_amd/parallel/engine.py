@@ -372,6 +372,11 @@ class FFNTrainer:
         return self._master if not self.split else self._join_master()
 
     @property
+    def master_numel(self) -> int:
+        """Elements of this rank's fp32 master state (without joining a split master)."""
+        return (self.master_lo if self.split else self._master).numel()
+
+    @property
     def master_bytes(self) -> int:
         """Bytes of master-weight state besides the working copy: the fp32 master, or the split format's residual
         plane."""
@@ -608,7 +613,9 @@ class FFNTrainer:
         self.side_sync()
         self.ddp_sync()
         self.fsdp_sync()
-        src = self.master if flat is None else flat
+        # split masters outside ZeRO: join each entry on its own (no full-size fp32 transient)
+        per_entry = flat is None and self.split and not self.zero
+        src = None if per_entry else (self.master if flat is None else flat)
         if self.zero:
             self.zero_sync_state()
             src = self.full_flat(src)
@@ -616,7 +623,8 @@ class FFNTrainer:
         for l in range(self.L):
             p = {}
             for name in ("w1", "w2"):
-                mv = self._view(src, self.entry[(l, name)])
+                e = self.entry[(l, name)]
+                mv = self.master_slice(e.offset, e.offset + e.numel).view(e.shape) if per_entry else self._view(src, e)
                 if self.fsdp:
                     full = torch.empty(self.entry[(l, name)].full_shape, dtype=torch.float32, device=self.device)
                     comm.all_gather_into(full, mv.contiguous(), self.mesh.group("dp_ag"), async_op=False)

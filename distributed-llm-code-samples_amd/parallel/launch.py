@@ -129,6 +129,9 @@ def run_rank(rank: int, world: int, cfg_dict: dict, method: int, backend: str, p
         raise
     timer.finish()
     eng.check_health()
+    # peak of training itself: read before the checkpoint export / parameter gather, which materialise transient
+    # full fp32 copies of split masters that never exist during a step
+    peak_hbm = torch.cuda.max_memory_allocated(device) / 2**30 if device.type == "cuda" else 0.0
     if opts.get("ckpt_dir"):
         save_checkpoint(eng, opts["ckpt_dir"], step=done, fmt=opts.get("ckpt_format", "consolidated"),
                         meta={"method": method, "seed": seed, "cfg": cfg_dict})
@@ -151,9 +154,9 @@ def run_rank(rank: int, world: int, cfg_dict: dict, method: int, backend: str, p
             "shapes": [(tuple(p["w1"].shape), tuple(p["w2"].shape)) for p in full] if full else None,
             "slices": [(p["w1"][:5, :5].clone(), p["w2"][:5, :5].clone()) for p in full] if full else None,
             "params": full if opts.get("return_full", False) else None,
-            "peak_hbm_gib": torch.cuda.max_memory_allocated(device) / 2**30 if device.type == "cuda" else 0.0,
+            "peak_hbm_gib": peak_hbm,
             # per-rank persistent state (elements): ZeRO keeps 1/dp of the fp32 master / moments
-            "state_numel": {"master": eng.master.numel(), "total": eng.total, "copy": eng.copy.numel(),
+            "state_numel": {"master": eng.master_numel, "total": eng.total, "copy": eng.copy.numel(),
                             "grads": eng.grads.numel(),
                             "adam": eng.adam_m.numel() if getattr(eng, "adam_m", None) is not None else 0},
             "ckpt_bytes_read_max": read_max,

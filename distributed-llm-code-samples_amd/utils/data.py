@@ -59,9 +59,11 @@ class DeviceMockData:
             return self.x, self.dy
         k = self._n % 2
         self._n += 1
-        if self._ready is not None and self._ready[:2] == (int(seed), k):
+        if self._ready is not None:
+            # order after the side-stream draw whether or not it is the batch asked for: on a mismatch (resume,
+            # skipped step, an eval fill) the redraw below may target the very slot that draw is still writing
             torch.cuda.current_stream(self.x.device).wait_event(self._ready[2])
-        else:
+        if self._ready is None or self._ready[:2] != (int(seed), k):
             self._draw(*self._slots[k], seed)
         self._ready = None
         self._pending = (int(next_seed), k ^ 1) if next_seed is not None else None

@@ -56,3 +56,35 @@ def test_bench_side_methods_deadline_keeps_headline(free_port):
     rec = _run(free_port, "--side_deadline_s", "0.05")
     assert "cut off" in rec["note"]
     assert any("error" in m for m in rec["methods"].values())
+
+
+def test_bench_self_launches_ranks():
+    """``python bench.py --gpus 2`` with no launcher starts its own two ranks (the reference starts one worker per GPU
+    from a plain ``python train_ffns.py``, train_ffns.py:184-191): one JSON line, world_size 2, every role
+    communicator of the headline spanning both ranks."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--backend", "gloo", "--model_size", "64", "--layers", "2", "--batch_size", "2", "--seq_len", "16",
+           "--dtype", "fp32", "--methods", "none"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["PYTHONPATH"] = ROOT
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert KEYS <= set(rec)
+    assert rec["n_gpus"] == 2 and rec["world_size"] == 2 and rec["launcher"] == "self"
+    assert rec["config"]["parallelism"] == "dp2-zero2" and rec["config"]["global_batch"] == 4
+    assert rec["comm_sizes"] and all(v == 2 for v in rec["comm_sizes"].values()), rec["comm_sizes"]
+
+
+def test_bench_self_launch_propagates_rank_failure():
+    """A rank that dies fails the whole self-launched run (non-zero exit), instead of hanging or printing a line."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--backend", "gloo", "--model_size", "64", "--layers", "2", "--batch_size", "2", "--seq_len", "16",
+           "--dtype", "fp32", "--methods", "none", "--no_such_flag"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["PYTHONPATH"] = ROOT
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert r.returncode != 0
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]

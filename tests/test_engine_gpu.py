@@ -332,3 +332,25 @@ def test_overlapped_data_pipeline_bitwise():
         outs.append(eng.master.clone())
     assert torch.isfinite(outs[0]).all()
     assert torch.equal(outs[0], outs[1])
+
+
+def test_overlapped_data_mismatched_seed_bitwise():
+    """A fill whose seed differs from the announced next_seed (resume, skipped step, eval fill) waits for the
+    in-flight side-stream draw before redrawing, so it returns exactly the synchronous draw of that seed even when
+    the side stream is still writing the same slot (the redraw used to race the prefetch)."""
+    from dllm.utils.data import DeviceMockData
+
+    T, D = 8192, 4096
+    dev = torch.device("cuda")
+    ref = DeviceMockData(T, D, torch.bfloat16, dev)
+    data = DeviceMockData(T, D, torch.bfloat16, dev, overlap=True)
+    for s in range(4):
+        x, dy = data.fill(100 + s, next_seed=777)  # announces 777, then asks for 101, 102, ...
+        data.release()                             # side stream starts drawing 777 into the other slot
+        rx, rdy = ref.fill(100 + s)
+        torch.cuda.synchronize()
+        assert torch.equal(x, rx) and torch.equal(dy, rdy), s
+    x, dy = data.fill(777)                          # the announced seed is still served from the prefetch
+    rx, rdy = ref.fill(777)
+    torch.cuda.synchronize()
+    assert torch.equal(x, rx) and torch.equal(dy, rdy)
