@@ -213,6 +213,18 @@ def parse(argv=None):
                    help="diagnostic: create the process group before the N=1 headline (as N>1 runs must)")
     p.add_argument("--force_comm", action="store_true",
                    help="exercise the RCCL DDP/FSDP path of the headline at N=1 (size-1 communicators)")
+    p.add_argument("--hw_queues", type=int, default=0,
+                   help="GPU_MAX_HW_QUEUES for this run (HIP hardware queues per process; 0 = leave HIP's setting, "
+                        "default 4).  Set before the first HIP call; self-launched ranks inherit it")
+    p.add_argument("--no_queue_reserve", action="store_true",
+                   help="do not reserve the compute stream's hardware queue at start (utils/streams.py)")
+    p.add_argument("--diff_pairs", type=int, default=3,
+                   help="communicating methods: interleaved pairs of (--diff_steps normal steps, --diff_steps steps with "
+                        "every collective elided); exposed_ms_diff = median normal - median elided step time")
+    p.add_argument("--diff_steps", type=int, default=4)
+    p.add_argument("--no_pair_wgrads", action="store_true",
+                   help="run small-grid weight-gradient pairs (the MP / TP8 shard) as two split-K GEMMs instead of one "
+                        "grouped launch")
     return p.parse_args(argv)
 
 
@@ -327,6 +339,15 @@ def _run_on_mesh(a, method, cfg, mesh, n, world, dev, steps, warmup, force_comm,
 
     for i in range(warmup):
         one_step(seed_base + i)
+    queues = None
+    if not cpu and a.backend == "nccl":
+        # every stream of this method exists and has run by now: measure which share the compute stream's queue
+        from dllm.utils.streams import queue_report
+
+        sync()
+        queues = queue_report(dev, {"wgrad": eng.wg_stream, "opt": getattr(eng, "opt_stream", None),
+                                    "fsdp": getattr(eng, "fsdp_stream", None),
+                                    "data": getattr(data, "_stream", None)})
     if a.phases and headline and not cpu and graphed is None:
         eng.enable_phase_timing(True)
     sync()
@@ -358,14 +379,48 @@ def _run_on_mesh(a, method, cfg, mesh, n, world, dev, steps, warmup, force_comm,
            "comm_sizes": {role: g.size() for role, g in mesh.groups.items() if g is not None}}
     if phases:
         rec["phase_ms_per_step"] = phases
+    if queues is not None:
+        rec["queues"] = queues
     communicates = bool(mesh.groups) or eng.tp_car is not None
+    nxt = seed_base + warmup + steps
     if observe_steps > 0 and communicates and not cpu and graphed is None:
         from dllm.utils.observe import CommObserver
 
         with CommObserver(dev, dict(mesh.groups)) as obs:
             for i in range(observe_steps):
-                one_step(seed_base + warmup + steps + i)
+                one_step(nxt + i)
+        nxt += observe_steps
         rec["comm"] = obs.summary(observe_steps)
+    if a.diff_pairs > 0 and a.diff_steps > 0 and communicates and graphed is None:
+        # differential exposed communication: the same engine with its collectives elided (compute only), interleaved
+        # with normal steps in this process; the difference of the medians is the step time the collectives add
+        on, off = [], []
+        for _ in range(a.diff_pairs):
+            for elide, acc in ((False, on), (True, off)):
+                old = comm.set_elide(elide)
+                try:
+                    sync()
+                    comm.barrier(device=dev)
+                    t1 = time.perf_counter()
+                    for i in range(a.diff_steps):
+                        one_step(nxt + i)
+                    sync()
+                    comm.barrier(device=dev)
+                    dt = time.perf_counter() - t1
+                finally:
+                    comm.set_elide(old)
+                nxt += a.diff_steps
+                if world > 1:
+                    import torch.distributed as dist
+
+                    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+                    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                    dt = float(t.item())
+                acc.append(dt / a.diff_steps * 1e3)
+        med = lambda v: sorted(v)[len(v) // 2]  # noqa: E731
+        c = rec.setdefault("comm", {})
+        c["exposed_ms_diff"] = round(med(on) - med(off), 3)
+        c["diff_step_ms"] = {"normal": [round(v, 3) for v in on], "collectives_elided": [round(v, 3) for v in off]}
     if eng.zero:
         eng.zero_sync_state()  # quiesce in-flight weight all-gathers before teardown
     sync()
@@ -378,11 +433,13 @@ def _run_on_mesh(a, method, cfg, mesh, n, world, dev, steps, warmup, force_comm,
 
 
 SIDE_KEYS = ("value", "ms_per_step", "tflops_per_gpu", "peak_hbm_gib", "parallelism", "model", "global_batch",
-             "steps", "finite", "state_gib", "comm")
+             "steps", "finite", "state_gib", "comm", "queues", "comm_sizes")
 
 
 def main(argv=None) -> int:
     a = parse(argv)
+    if a.hw_queues > 0:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(a.hw_queues)   # read by HIP at its first call, which is below
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     n = a.gpus or world
@@ -392,6 +449,11 @@ def main(argv=None) -> int:
     methods = [m for m in a.methods.split(",") if m and m != "none"]
     if not cpu:
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count()))
+        if not a.no_queue_reserve:
+            # before any process group / RCCL communicator / torch stream pool exists (utils/streams.py)
+            from dllm.utils.streams import reserve_compute_queue
+
+            reserve_compute_queue(torch.cuda.current_device())
     def init_dist():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
@@ -416,9 +478,10 @@ def main(argv=None) -> int:
 
         set_bf16_variant(a.gemm_variant)
     if not cpu:
-        from dllm.ops.gemm import set_group_m_nt
+        from dllm.ops.gemm import set_group_m_nt, set_pair_wgrads
 
         set_group_m_nt(a.group_m_nt)
+        set_pair_wgrads(not a.no_pair_wgrads)
     ffn = a.ffn_dim or (a.mp_ffn_dim if a.method == "tp" else 0)
     model = ModelConfig(model_size=a.model_size, ffn_dim=ffn, layers=a.layers, act=a.act, gated=a.gated)
     head = run_method(a, a.method, n, world, dev, a.steps, a.warmup, a.force_comm, model,
@@ -449,7 +512,7 @@ def main(argv=None) -> int:
             "comm_backend": a.comm, "hip_graph": bool(a.graph), "gemm_variant": a.gemm_variant,
             "tp_allreduce": a.tp_allreduce, "wgrad_stream": head.get("wgrad_stream", False),
         }
-        for k in ("comm", "phase_ms_per_step"):
+        for k in ("comm", "phase_ms_per_step", "queues"):
             if k in head:
                 rec[k] = head[k]
         if side:

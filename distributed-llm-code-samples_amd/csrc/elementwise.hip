@@ -298,6 +298,19 @@ __global__ void occupy_kernel(long ticks, float* sink) {
   if (acc == -1.f) sink[threadIdx.x] = acc;  // never true; keeps the loop
 }
 
+// Hardware-queue probe: one wave spins ``ticks`` of the 100 MHz realtime counter, then lane 0 records [start, end]
+// (vector stores).  Two of these on two streams tell whether the streams share a hardware queue: a queue runs its
+// dispatches in order, so the second one's start lands after the first one's end only when they share it.
+__global__ void stamp_kernel(unsigned long long* out, long ticks) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  uint64_t t = t0;
+  while ((long)(t - t0) < ticks) t = __builtin_amdgcn_s_memrealtime();
+  if (out != nullptr && threadIdx.x == 0) {
+    out[0] = t0;
+    out[1] = t;
+  }
+}
+
 static inline int grid_for(long n4) {
   long g = (n4 + 255) / 256;
   if (g > 2048) g = 2048;
@@ -422,6 +435,52 @@ int dllm_occupy(int blocks, int threads, float us, float* sink, void* stream) {
   return (int)hipGetLastError();
 }
 
-int dllm_abi_version() { return 8; }
+// 1: ``probe`` runs on the hardware queue of ``base`` (its stamp starts after base's spin ends), 0: a queue of its
+// own, < 0: error.  Both streams are synchronised.
+int dllm_queue_shared(void* base, void* probe, int spin_us) {
+  static unsigned long long* buf = nullptr;
+  if (!buf && hipMalloc(&buf, 64) != hipSuccess) return -2;
+  hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(64), 0, (hipStream_t)base, buf, (long)spin_us * 100);
+  hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(64), 0, (hipStream_t)probe, buf + 2, 0L);
+  if (hipGetLastError() != hipSuccess) return -3;
+  if (hipStreamSynchronize((hipStream_t)base) != hipSuccess || hipStreamSynchronize((hipStream_t)probe) != hipSuccess)
+    return -4;
+  unsigned long long h[4];
+  if (hipMemcpy(h, buf, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess) return -5;
+  return h[2] >= h[1] ? 1 : 0;
+}
+
+// Reserve ``base``'s hardware queue for it.  HIP gives a process GPU_MAX_HW_QUEUES queues per priority and puts each
+// new stream on the least-used one, so any stream created later (torch's pool, which ProcessGroupNCCL / RCCL and the
+// engine's side streams draw from) can land on the compute stream's queue and serialise with it
+// (profiles/r3/hw_queue_collision_trace_r3.txt).  Here ``candidates`` non-blocking streams are created and used one by
+// one; those that landed on base's queue are kept for the process (blockers: they raise that queue's use count) and
+// the others destroyed, so later streams fill the other queues first.  Returns the number of blockers (< 0: error).
+int dllm_queue_reserve(void* base, int candidates, int spin_us) {
+  static hipStream_t blockers[512];
+  static int nblock = 0;
+  if (candidates <= 0 || candidates > 512) return -1;
+  hipStream_t cand[512];
+  int made = 0;
+  for (int i = 0; i < candidates; ++i) {
+    if (hipStreamCreateWithFlags(&cand[i], hipStreamNonBlocking) != hipSuccess) break;
+    made = i + 1;
+    // first use of a stream acquires its queue: do that before the timed probe, so a slow queue creation is not
+    // mistaken for sharing
+    hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(64), 0, cand[i], (unsigned long long*)nullptr, -1L);
+    if (hipStreamSynchronize(cand[i]) != hipSuccess) return -6;
+    const int sh = dllm_queue_shared(base, (void*)cand[i], spin_us);
+    if (sh < 0) return sh;
+    if (sh == 1 && nblock < 512) {
+      blockers[nblock++] = cand[i];
+      cand[i] = nullptr;
+    }
+  }
+  for (int i = 0; i < made; ++i)
+    if (cand[i]) hipStreamDestroy(cand[i]);
+  return nblock;
+}
+
+int dllm_abi_version() { return 9; }
 
 }  // extern "C"

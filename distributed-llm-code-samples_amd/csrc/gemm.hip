@@ -111,6 +111,50 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
   return (int)e;
 }
 
+// Two TN (weight-gradient) GEMMs of one epilogue and one K in a single grouped launch, one 256x256 tile per block
+// (gemm_bf16_8ph_pair).  Per-problem arrays of 2: A, lda, B, ldb, C, ldc, aux_out, ldaux, opt_m, opt_v, M, N.  Returns
+// -1 when the pair does not fit the grouped kernel (the caller then runs two dllm_gemm calls): bf16 operands, both
+// shapes 256-tiled, K % 128 == 0, 16-B aligned, and tiles(0) + tiles(1) <= the device's CUs.
+int dllm_gemm_pair(int out_dtype, int epi, const void* const* A, const long* lda, const void* const* B,
+                   const long* ldb, void* const* C, const long* ldc, void* const* aux_out, const long* ldaux,
+                   float* const* opt_m, float* const* opt_v, const int* M, const int* N, int K, float alpha,
+                   float lr, float b1, float b2, float eps, float wd, int step, void* stream) {
+  if (K <= 0 || K % (2 * BT_K) != 0) return -1;
+  if (epi != EPI_STORE && epi != EPI_SGD && epi != EPI_SGDS && epi != EPI_ADAM && epi != EPI_ADAMS) return -1;
+  const bool split_epi = (epi == EPI_SGDS || epi == EPI_ADAMS);
+  if ((epi == EPI_SGD || epi == EPI_ADAM) && out_dtype != DT_F32) return -1;
+  if (split_epi && out_dtype != DT_BF16) return -1;
+  GemmArgs a[2];
+  int tiles = 0;
+  for (int i = 0; i < 2; ++i) {
+    if (M[i] <= 0 || N[i] <= 0 || M[i] % BT_M || N[i] % BT_N) return -1;
+    if (split_epi && aux_out[i] == nullptr) return -1;
+    if ((epi == EPI_ADAM || epi == EPI_ADAMS) && (step < 1 || !opt_m[i] || !opt_v[i])) return -1;
+    const bool al = ((uintptr_t)A[i] % 16 == 0) && ((uintptr_t)B[i] % 16 == 0) && ((uintptr_t)C[i] % 16 == 0) &&
+                    ((uintptr_t)aux_out[i] % 16 == 0) && ((uintptr_t)opt_m[i] % 16 == 0) &&
+                    ((uintptr_t)opt_v[i] % 16 == 0) && lda[i] % 8 == 0 && ldb[i] % 8 == 0 && ldc[i] % 4 == 0 &&
+                    ldaux[i] % 4 == 0 && (!split_epi || (ldc[i] % 8 == 0 && ldaux[i] % 8 == 0));
+    if (!al) return -1;
+    GemmArgs& g = a[i];
+    g = GemmArgs{};
+    g.A = A[i]; g.B = B[i]; g.C = C[i]; g.aux = nullptr; g.aux_out = aux_out[i];
+    g.lda = lda[i]; g.ldb = ldb[i]; g.ldc = ldc[i]; g.ldaux = ldaux[i];
+    g.M = M[i]; g.N = N[i]; g.K = K; g.alpha = alpha; g.beta = 0.f; g.act = ACT_NONE; g.group_m = 4;
+    g.lr = lr; g.b1 = b1; g.b2 = b2; g.eps = eps; g.wd = wd; g.opt_m = opt_m[i]; g.opt_v = opt_v[i];
+    g.bc1 = 1.f; g.bc2 = 1.f;
+    if (epi == EPI_ADAM || epi == EPI_ADAMS) {
+      g.bc1 = 1.f - powf(b1, (float)step);
+      g.bc2 = 1.f - powf(b2, (float)step);
+    }
+    g.ksplit = 1; g.tpb = 1; g.variant = 3; g.tpb_req = 1; g.min_bpc = 1; g.ws = nullptr; g.mask = nullptr;
+    g.skew = 0;
+    tiles += (M[i] / BT_M) * (N[i] / BT_N);
+  }
+  const int ncu = num_cu();
+  if (ncu <= 0 || tiles > ncu) return -1;
+  return (int)dispatch_tn_pair(epi, a[0], a[1], out_dtype, (hipStream_t)stream);
+}
+
 // which kernel family dllm_gemm would pick (for tests / profiling labels)
 int dllm_gemm_path(int in_dtype, int out_dtype, int M, int N, int K, long lda, long ldb, long ldc) {
   const bool al = (lda % 8 == 0) && (ldb % 8 == 0) && (ldc % 4 == 0);  // (bases: checked per call)

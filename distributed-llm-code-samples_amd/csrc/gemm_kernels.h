@@ -952,9 +952,10 @@ __device__ __forceinline__ bf16x8_t cat_tr(s16x4_t lo, s16x4_t hi) {
 // does not rematerialise kernarg loads, so arguments used only by a persistent kernel's per-tile epilogue
 // would otherwise stay live in SGPRs across the main loop (and spill).  The empty asm makes the pointer
 // opaque so the loads cannot be hoisted.
-__device__ __forceinline__ GemmArgs reload_args() {
+// ``which`` selects the argument block of a grouped launch (gemm_bf16_8ph_pair: two GemmArgs back to back).
+__device__ __forceinline__ GemmArgs reload_args(int which = 0) {
   typedef const __attribute__((address_space(4))) uint32_t* KargWords;
-  KargWords pa = (KargWords)__builtin_amdgcn_kernarg_segment_ptr();
+  KargWords pa = (KargWords)__builtin_amdgcn_kernarg_segment_ptr() + which * (int)(sizeof(GemmArgs) / 4);
   asm volatile("" : "+s"(pa));
   struct Words { uint32_t w[sizeof(GemmArgs) / 4]; } r;
 #pragma unroll
@@ -972,8 +973,10 @@ __device__ __forceinline__ GemmArgs reload_args() {
 // NPH = 8: the 8-phase schedule below (one quadrant = 16 MFMAs per wave per barrier interval).
 // NPH = 4: half-tile phases (two quadrants = 32 MFMAs per interval, two half-tiles restaged per phase):
 // halves the barrier count per MFMA (see the NPH == 4 loop).
-template <int LAYOUT, int EPI, typename OutT, bool STAGGER, int ACT = -1, int NPH = 8, bool PERS = false>
-__global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
+// GRP: one block of a grouped launch (gemm_bf16_8ph_pair): ``p`` is argument block ``which`` of the kernel, ``slot0``
+// the block's tile in that problem (already XCD-remapped over the whole grid); one tile per block.
+template <int LAYOUT, int EPI, typename OutT, bool STAGGER, int ACT, int NPH, bool PERS, bool GRP>
+__device__ __forceinline__ void gemm_8ph_body(const GemmArgs& p, const int which, const int slot0) {
   // slot(op, hh, buf) = ((op*2 + hh)*2 + buf) * 16 KiB: A in [0, 64K), B in [64K, 128K), so every
   // fragment read is base + a 16-bit immediate
   __shared__ __attribute__((aligned(16))) char smem[8 * HT];
@@ -988,14 +991,14 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
   // a multiple of the 8 XCDs, so every slot of a block maps to the block's own XCD under the remap).  Slot ->
   // tile goes through the XCD remap over ALL slots: the same tile placement and order as one block per tile.
   // A separate instantiation, so the one-tile-per-block kernels carry none of its state.
-  const bool pers = PERS && NPH == 8 && p.tpb > 1;
-  int slot = blockIdx.x;
+  const bool pers = PERS && !GRP && NPH == 8 && p.tpb > 1;
+  int slot = slot0;
   // Per-slot helpers take the argument block explicitly: inside the slot loop they are called with a fresh
   // reload_args() copy, so the epilogue's arguments are loaded where they are used instead of being kept
   // live in SGPRs across the whole main loop.
   auto tile_of = [&](const GemmArgs& q, int s, int& sp, int& tm0, int& tn0) {
     const int tm_ = q.M / BT_M, tn_ = q.N / BT_N, nt = tm_ * tn_;
-    const int bid0 = xcd_remap(s, pers ? nt * q.ksplit : (int)gridDim.x);
+    const int bid0 = GRP ? s : xcd_remap(s, pers ? nt * q.ksplit : (int)gridDim.x);
     sp = bid0 / nt;  // split-K slice (0 when ksplit == 1)
     const int bid = bid0 % nt;
     const int width = q.group_m * tn_;
@@ -1029,7 +1032,7 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
   };
   // epilogue of a slot; split-K slices write fp32 partial planes C + split*M*ldc
   auto slot_epilogue = [&](int s, f32x4_t (&ac)[2][2][4][2]) {
-    const GemmArgs q = reload_args();
+    const GemmArgs q = reload_args(which);
     int sp, tm0, tn0;
     tile_of(q, s, sp, tm0, tn0);
     void* out = q.C;
@@ -1262,7 +1265,7 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
     if (it == nk / 2 - 1) {
       // last iteration: the remaining prefetches are the next slot's K-tiles 0/1 (or harmless re-loads)
       if (next_slot < total) {
-        const GemmArgs q = reload_args();
+        const GemmArgs q = reload_args(which);
         Apf = a_base(q, next_slot);
         Bpf = b_base(q, next_slot);
       } else {
@@ -1341,6 +1344,24 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
   // drain the tail prefetches before the block can release its LDS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   slot_epilogue(slot, acc);
+}
+
+template <int LAYOUT, int EPI, typename OutT, bool STAGGER, int ACT = -1, int NPH = 8, bool PERS = false>
+__global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
+  gemm_8ph_body<LAYOUT, EPI, OutT, STAGGER, ACT, NPH, PERS, false>(p, 0, blockIdx.x);
+}
+
+// Two GEMMs of one layout, epilogue and K in ONE launch, one 256x256 tile per block (grid = tiles(p0) + tiles(p1)
+// <= CUs).  For weight-gradient pairs whose own grids leave the chip part-empty -- the MP (TP8) shard's dW2 [D, F/8]
+// and dW1 [F/8, D], 112 tiles each at F = 14336 -- instead of split-K slices and a reduction pass per GEMM.  The
+// remapped block ids are split [0, tiles(p0)) | [tiles(p0), ...), so each problem's tiles fill whole XCDs of their own
+// (no operand panel is shared across the two problems) and keep the grouped raster inside the problem.
+template <int LAYOUT, int EPI, typename OutT>
+__global__ __launch_bounds__(512, 2) void gemm_bf16_8ph_pair(GemmArgs p0, GemmArgs p1) {
+  const int nt0 = (p0.M / BT_M) * (p0.N / BT_N);
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int which = bid >= nt0 ? 1 : 0;  // one inlined body over the selected argument block (code size)
+  gemm_8ph_body<LAYOUT, EPI, OutT, true, -1, 8, false, true>(which ? p1 : p0, which, bid - which * nt0);
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -2016,10 +2037,19 @@ static hipError_t dispatch_opt(int path, const GemmArgs& a, int in_dt, hipStream
 }
 
 
+// grouped weight-gradient pair (gemm_bf16_8ph_pair): TN layout, one tile per block, any wgrad epilogue
+template <int E, typename OutT>
+static hipError_t launch_pair(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s) {
+  const int nb = (a0.M / BT_M) * (a0.N / BT_N) + (a1.M / BT_M) * (a1.N / BT_N);
+  hipLaunchKernelGGL((gemm_bf16_8ph_pair<L_TN, E, OutT>), dim3(nb), dim3(512), 0, s, a0, a1);
+  return hipGetLastError();
+}
+
 // per-layout entry points (one translation unit each)
 hipError_t dispatch_nt(int path, int epi, const GemmArgs& a, int in_dt, int out_dt, hipStream_t s);
 hipError_t dispatch_nn(int path, int epi, const GemmArgs& a, int in_dt, int out_dt, hipStream_t s);
 hipError_t dispatch_tn(int path, int epi, const GemmArgs& a, int in_dt, int out_dt, hipStream_t s);
 hipError_t dispatch_tn_opt(int path, int epi, const GemmArgs& a, int in_dt, hipStream_t s);
+hipError_t dispatch_tn_pair(int epi, const GemmArgs& a0, const GemmArgs& a1, int out_dt, hipStream_t s);
 
 }  // namespace dllm

@@ -24,7 +24,7 @@ from __future__ import annotations
 
 import torch
 
-from ..ops.gemm import gemm
+from ..ops.gemm import gemm, gemm_pair
 from ..utils.config import INIT_SCALE
 
 GLU_BLOCK = 16
@@ -111,7 +111,7 @@ def layer_fwd(x: torch.Tensor, w1: torch.Tensor, w2: torch.Tensor, act: str, gat
 def layer_bwd(dy: torch.Tensor, x: torch.Tensor, w1: torch.Tensor, w2: torch.Tensor, act: str, gated: bool,
               a: torch.Tensor, h: torch.Tensor | None, gw1, gw2, da_buf: torch.Tensor,
               dx_out: torch.Tensor | None, hooks=None, mask: torch.Tensor | None = None,
-              dx_first: bool = False) -> torch.Tensor | None:
+              dx_first: bool = False, pair_wgrads: bool = False) -> torch.Tensor | None:
     """Backward of one layer; returns dx.
 
     ``gw1``/``gw2`` are either gradient tensors (overwritten) or dicts of ``gemm`` keyword arguments for the
@@ -124,6 +124,10 @@ def layer_bwd(dy: torch.Tensor, x: torch.Tensor, w1: torch.Tensor, w2: torch.Ten
     ``da, dx, dW2, dW1`` -- the input-gradient all-reduce, on which the next layer's whole backward waits,
     then overlaps BOTH weight-gradient GEMMs.  Without ``dx`` (layer 0) the order is ``da, dW1, dW2`` (the
     engine's flat layout follows the completion order).
+
+    ``pair_wgrads`` (small tile grids, e.g. the MP / TP8 shard): ``da, dx, (dW2 | dW1)`` -- both weight gradients
+    in ONE grouped launch (``ops.gemm.gemm_pair``) that fills the chip with whole tiles instead of two split-K GEMMs
+    and their reduction passes; dx still runs before W1's fused update, and a TP all-reduce of dx overlaps the pair.
     """
     if gated:
         gemm(dy, w2, "nn", out=da_buf, epi="dglu", act=act, aux=h)    # [dg|du] interleaved [T, 2F]
@@ -131,6 +135,21 @@ def layer_bwd(dy: torch.Tensor, x: torch.Tensor, w1: torch.Tensor, w2: torch.Ten
         gemm(dy, w2, "nn", out=da_buf, epi="dact", act=act, aux=h if h is not None else a, mask=mask)
     kw1 = gw1 if isinstance(gw1, dict) else {"out": gw1}
     kw2 = gw2 if isinstance(gw2, dict) else {"out": gw2}
+    if pair_wgrads:
+        dx = None
+        if dx_out is not None:
+            dx = gemm(da_buf, w1, "nn", out=dx_out)                   # dx = da·W1 (before W1's update)
+            if hooks is not None:
+                hooks.after_dx(dx)
+        gemm_pair(dy, a, kw2, da_buf, x, kw1)                          # dW2 = dyᵀ·a  |  dW1 = daᵀ·x
+        if hooks is not None:
+            if dx_out is None:   # layer 0's completion order (flat layout): W1 first
+                hooks.after_w1()
+                hooks.after_w2()
+            else:
+                hooks.after_w2()
+                hooks.after_w1()
+        return dx
     if dx_out is None:
         # no input gradient (layer 0): dW1 first, so W1's gradient collective / update starts while dW2
         # runs and the next forward's first GEMM (which needs W1) is not behind the step's last collective

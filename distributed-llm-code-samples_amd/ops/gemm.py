@@ -336,6 +336,97 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
     return out
 
 
+_PAIR = {"enabled": True}
+
+
+def set_pair_wgrads(enabled: bool) -> bool:
+    """Allow grouped weight-gradient pairs (``gemm_pair``); returns the previous setting."""
+    old = _PAIR["enabled"]
+    _PAIR["enabled"] = bool(enabled)
+    return old
+
+
+def pair_supported(shapes, dtype: torch.dtype = torch.bfloat16) -> bool:
+    """Whether two TN GEMMs ``shapes = ((M0, N0, K), (M1, N1, K))`` run as one grouped launch: bf16, 256-tiled, the
+    8-phase K step, both tile grids together <= the CUs, and each alone small enough that it would run split-K (a
+    part-empty chip plus a reduction pass) -- e.g. the MP (TP8) shard's dW2 [4096, 1792] and dW1 [1792, 4096]."""
+    (M0, N0, K0), (M1, N1, K1) = shapes
+    if not _PAIR["enabled"] or dtype != torch.bfloat16 or K0 != K1 or K0 % 128:
+        return False
+    if any(m % 256 or n % 256 for m, n in ((M0, N0), (M1, N1))):
+        return False
+    if _VARIANT["name"] not in ("auto", "8phase_stagger"):
+        return False
+    tiles = (M0 // 256) * (N0 // 256) + (M1 // 256) * (N1 // 256)
+    return tiles <= NUM_CUS and (choose_ksplit(M0, N0, K0) > 1 or choose_ksplit(M1, N1, K1) > 1)
+
+
+def gemm_pair(a0: torch.Tensor, b0: torch.Tensor, kw0: dict, a1: torch.Tensor, b1: torch.Tensor, kw1: dict) -> None:
+    """Two weight-gradient (TN) GEMMs ``gemm(a0, b0, "tn", **kw0)`` and ``gemm(a1, b1, "tn", **kw1)`` -- same epilogue
+    and K -- as ONE grouped launch with one 256x256 tile per block (``csrc/gemm_kernels.h`` ``gemm_bf16_8ph_pair``).
+    Each result is bitwise the unsplit single GEMM's.  Falls back to two ``gemm`` calls where the grouped kernel does
+    not apply (CPU tensors, shapes, alignment)."""
+    M0, N0, K0 = gemm_shape(a0, b0, "tn")
+    M1, N1, K1 = gemm_shape(a1, b1, "tn")
+    epi = kw0.get("epi", "store")
+    if a0.device.type != "cuda" or kw1.get("epi", "store") != epi or not pair_supported(((M0, N0, K0), (M1, N1, K1)),
+                                                                                         a0.dtype):
+        gemm(a0, b0, "tn", **kw0)
+        gemm(a1, b1, "tn", **kw1)
+        return
+    for kw in (kw0, kw1):
+        bad = set(kw) - {"out", "epi", "lr", "aux_out", "betas", "eps", "wd", "step", "opt_m", "opt_v", "alpha"}
+        if bad or kw.get("out") is None:
+            raise ValueError(f"gemm_pair: unsupported arguments {sorted(bad) or ['out missing']}")
+        for k in ("lr", "betas", "eps", "wd", "step", "alpha"):
+            if kw.get(k) != kw0.get(k):
+                raise ValueError(f"gemm_pair: both GEMMs must share {k}")
+    outs = [kw0["out"], kw1["out"]]
+    for (M, N), o in zip(((M0, N0), (M1, N1)), outs):
+        if o.shape != (M, N):
+            raise ValueError(f"gemm_pair: out {tuple(o.shape)} != {(M, N)}")
+    for t, nm in ((a0, "a0"), (b0, "b0"), (a1, "a1"), (b1, "b1"), *((o, "out") for o in outs)):
+        _check_rowmajor(t, nm)
+    if epi in ("sgd", "adam") and any(o.dtype != torch.float32 for o in outs):
+        raise ValueError("fused-optimizer epilogues need an fp32 master")
+    if epi in ("sgd_split", "adam_split") and any(o.dtype != torch.int16 or kw.get("aux_out") is None
+                                                  for o, kw in zip(outs, (kw0, kw1))):
+        raise ValueError(f"{epi} needs int16 residual planes and bf16 working copies")
+    from ctypes import c_float, c_int, c_long, c_void_p
+
+    def arr(ctype, vals):
+        return (ctype * 2)(*vals)
+
+    kws = (kw0, kw1)
+    aux = [kw.get("aux_out") for kw in kws]
+    om = [kw.get("opt_m") for kw in kws]
+    ov = [kw.get("opt_v") for kw in kws]
+    ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+    betas = kw0.get("betas", (0.9, 0.95))
+    out_dt = _native.dtype_code(torch.bfloat16 if outs[0].dtype == torch.int16 else outs[0].dtype)
+    L = _native.lib()
+    obs = _observe.active()
+    if obs is not None:
+        obs.gemm_begin()
+    rc = L.dllm_gemm_pair(out_dt, EPIS[epi], arr(c_void_p, [a0.data_ptr(), a1.data_ptr()]),
+                          arr(c_long, [a0.stride(0), a1.stride(0)]), arr(c_void_p, [b0.data_ptr(), b1.data_ptr()]),
+                          arr(c_long, [b0.stride(0), b1.stride(0)]), arr(c_void_p, [o.data_ptr() for o in outs]),
+                          arr(c_long, [o.stride(0) for o in outs]), arr(c_void_p, [ptr(t) for t in aux]),
+                          arr(c_long, [t.stride(0) if t is not None else 0 for t in aux]),
+                          arr(c_void_p, [ptr(t) for t in om]), arr(c_void_p, [ptr(t) for t in ov]),
+                          arr(c_int, [M0, M1]), arr(c_int, [N0, N1]), K0, c_float(float(kw0.get("alpha", 1.0))),
+                          c_float(float(kw0.get("lr", 0.0))), c_float(float(betas[0])), c_float(float(betas[1])),
+                          c_float(float(kw0.get("eps", 1e-8))), c_float(float(kw0.get("wd", 0.0))),
+                          int(kw0.get("step", 0)), _native.stream_ptr(a0.device))
+    if obs is not None:
+        obs.gemm_end()
+    if rc == -1:   # not expressible as one grouped launch (alignment, CU count): two GEMMs
+        gemm(a0, b0, "tn", **kw0)
+        gemm(a1, b1, "tn", **kw1)
+        return
+    _native.check(rc, f"dllm_gemm_pair({epi},{(M0, N0)},{(M1, N1)},K={K0})")
+
+
 def relu_mask_bytes(M: int, N: int) -> int:
     """Size of the ReLU bitmask of an ``[M, N]`` activation (8 KiB per 256x256 tile)."""
     return (M // 256) * (N // 256) * 8192

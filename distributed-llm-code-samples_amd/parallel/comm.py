@@ -33,6 +33,21 @@ class Done:
 
 
 _SERIALIZE = False
+_ELIDE = False
+
+
+def set_elide(flag: bool) -> bool:
+    """Timing mode for the differential exposed-communication measurement (bench.py ``exposed_ms_diff``): every
+    collective on a communicator returns at once without running, so a step costs its compute alone.  The results of
+    such steps are meaningless (gradients are not reduced, shards not gathered); only their time is used.  Returns
+    the previous setting."""
+    global _ELIDE
+    old, _ELIDE = _ELIDE, bool(flag)
+    return old
+
+
+def eliding() -> bool:
+    return _ELIDE
 
 
 def set_serialize(flag: bool) -> None:
@@ -112,6 +127,8 @@ def _issue(group, fn, moves: bool = True):
 
 
 def all_reduce(t: torch.Tensor, group, async_op: bool = True):
+    if _ELIDE and group is not None:
+        return Done()
     if group is not None and _native(group):
         w = _issue(group, lambda: group.all_reduce(t), _moves(group, t, t))
         return _finish(w, async_op) if (async_op or _SERIALIZE) else (w.wait(), Done())[1]
@@ -123,6 +140,8 @@ def all_reduce(t: torch.Tensor, group, async_op: bool = True):
 
 
 def all_gather_into(out: torch.Tensor, shard: torch.Tensor, group, async_op: bool = True):
+    if _ELIDE and group is not None:
+        return Done()
     if group is not None and _native(group):
         w = _issue(group, lambda: group.all_gather_into(out.view(-1), shard.reshape(-1)), _moves(group, out, shard))
         return _finish(w, async_op) if (async_op or _SERIALIZE) else (w.wait(), Done())[1]
@@ -139,6 +158,8 @@ def all_gather_into(out: torch.Tensor, shard: torch.Tensor, group, async_op: boo
 
 
 def reduce_scatter_into(out: torch.Tensor, full: torch.Tensor, group, async_op: bool = True):
+    if _ELIDE and group is not None:
+        return Done()
     if group is not None and _native(group):
         w = _issue(group, lambda: group.reduce_scatter_into(out.view(-1), full.reshape(-1)), _moves(group, out, full))
         return _finish(w, async_op) if (async_op or _SERIALIZE) else (w.wait(), Done())[1]
@@ -172,6 +193,8 @@ class _Many:
 def all_gather_into_many(pairs, group, async_op: bool = True):
     """All-gathers ``(out, shard)`` issued as ONE group: the native layer fuses them with
     ncclGroupStart/End (one launch, one completion event); torch / gloo issue them back to back."""
+    if _ELIDE and group is not None:
+        return Done()
     if group is not None and _native(group) and not _SERIALIZE:
         w = _issue(group, lambda: group.all_gather_into_many([(o.view(-1), sh.reshape(-1)) for o, sh in pairs]),
                    any(_moves(group, o, sh) for o, sh in pairs))
@@ -182,6 +205,8 @@ def all_gather_into_many(pairs, group, async_op: bool = True):
 
 def reduce_scatter_into_many(pairs, group, async_op: bool = True):
     """Reduce-scatters ``(out, full)`` issued as ONE group (see ``all_gather_into_many``)."""
+    if _ELIDE and group is not None:
+        return Done()
     if group is not None and _native(group) and not _SERIALIZE:
         w = _issue(group, lambda: group.reduce_scatter_into_many([(o.view(-1), f.reshape(-1)) for o, f in pairs]),
                    any(_moves(group, o, f) for o, f in pairs))

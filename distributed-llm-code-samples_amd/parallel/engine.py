@@ -321,11 +321,19 @@ class FFNTrainer:
         # GEMMs fill each other's last tile wave (flagship D4096: 4 per CU, 0.4-1.1 % faster); with many tiles per CU
         # nothing is left to fill and the two concurrent GEMMs only split L2 / MALL (D8192 F32768, 16 per CU: 131.5 vs
         # 117.8 ms serial; profiles/r3/wgrad_stream_tiles_per_cu_r3.txt)
+        # grouped weight-gradient pair (small tile grids: the MP / TP8 shard's dW2 [D, F/8] and dW1 [F/8, D] would each
+        # run split-K plus a reduction pass): both in one launch of whole tiles, after dx (models/ffn.layer_bwd).  It
+        # replaces the weight-gradient stream there: two part-empty grids have no tail worth filling
+        self.pair_wgrads = False
+        if dev.type == "cuda":
+            from ..ops.gemm import pair_supported
+
+            self.pair_wgrads = pair_supported(((D, self.F_loc, T), (self.R1, D, T)), self.cd)
         self.wg_stream = None
         wg_tiles = -(-self.R1 // 256) * -(-D // 256)
         ncu = torch.cuda.get_device_properties(dev).multi_processor_count if dev.type == "cuda" else 256
         if (cfg.wgrad_stream and self.fused_opt and dev.type == "cuda" and not self.tp_comm and not self.sp
-                and cfg.recompute == "none" and wg_tiles <= cfg.wgrad_stream_max_tpc * ncu):
+                and cfg.recompute == "none" and wg_tiles <= cfg.wgrad_stream_max_tpc * ncu and not self.pair_wgrads):
             self.wg_stream = self._side_stream("wgrad")
             self.da_ring = [self.da, torch.empty_like(self.da)]
             self.da_free = [None, None]
@@ -1029,7 +1037,7 @@ class FFNTrainer:
                 hooks_sp = _SPHooks(self, l)
                 dxp = layer_bwd(self.dyfull, xin, w1, w2, act, gated, a, h, gw1, gw2, self.da,
                                 self.dxb[l % 2] if need_dx else None, hooks_sp, mask=self._mask(l),
-                                dx_first=cfg.tp_overlap)
+                                dx_first=cfg.tp_overlap, pair_wgrads=self.pair_wgrads)
                 if dxp is not None:
                     for w in hooks_sp.rs_work or ():
                         w.wait()
@@ -1041,7 +1049,7 @@ class FFNTrainer:
                     recompute_fwd1(self.xs[l], w1, act, gated, a, h, mask=self._mask(l))
                 dx = layer_bwd(g, self.xs[l], w1, w2, act, gated, a, h, gw1, gw2, self.da,
                                self.dxb[l % 2] if need_dx else None, hooks, mask=self._mask(l),
-                               dx_first=self.tp_comm and cfg.tp_overlap)
+                               dx_first=self.tp_comm and cfg.tp_overlap, pair_wgrads=self.pair_wgrads)
                 if dx is not None:
                     g = dx
             if self.zero:

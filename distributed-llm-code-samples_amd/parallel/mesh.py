@@ -46,6 +46,11 @@ def init_distributed(backend: str, rank: int | None = None, world_size: int | No
     if backend == "nccl":
         local = int(os.environ.get("LOCAL_RANK", rank))
         torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+        # keep RCCL's / the process groups' streams off the compute stream's hardware queue (utils/streams.py);
+        # must precede the communicators (idempotent: bench.py may have reserved already)
+        from ..utils.streams import reserve_compute_queue
+
+        reserve_compute_queue(torch.cuda.current_device())
         # eager communicator creation (device_id) unless DLLM_NCCL_EAGER=0: then RCCL builds it at the first collective
         if os.environ.get("DLLM_NCCL_EAGER", "1") != "0":
             kw["device_id"] = torch.device("cuda", torch.cuda.current_device())

@@ -20,6 +20,17 @@ stream can land on the compute stream's queue and the two streams' kernels seria
 More hardware queues are not the remedy: at 32 the hardware scheduler time-slices them and the communicating
 methods collapse (``profiles/r3/hw_queues_32_vs_16_r3.txt``); queues that own a CU mask cost 2 % on the headline
 (``profiles/r3/dedicated_cu_mask_queues_r3.txt``).  Native handles live for the process.
+
+**Reserving the compute stream's queue** (round 4, ``reserve_compute_queue``).  The compute stream is torch's default
+(HIP null) stream.  At process start, before torch's stream pool, any process group or RCCL communicator exists,
+``csrc/elementwise.hip: dllm_queue_reserve`` creates non-blocking candidate streams one by one and measures for each
+whether it landed on the compute stream's hardware queue (a spinning wave on the compute stream, a timestamp kernel on
+the candidate: a shared queue runs them in order).  Candidates on the compute queue are kept for the process, the
+others destroyed, so the compute queue carries the highest use count and HIP's least-used placement puts every later
+stream -- torch's pool (engine side streams, ProcessGroupNCCL's collective streams) and RCCL's own -- on the other
+queues.  ``queue_report`` re-measures any set of streams against the compute stream (bench.py reports it per method).
+Works at HIP's default of 4 queues per process; the package no longer changes ``GPU_MAX_HW_QUEUES`` (bench.py
+``--hw_queues`` sets it explicitly for a run).
 """
 from __future__ import annotations
 
@@ -32,6 +43,8 @@ import torch
 from .. import _native
 
 _native.register_optional("dllm_stream_create", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)])
+_RESERVED: dict[int, int] = {}
+PROBE_SPIN_US = 100
 _native.register_optional("dllm_stream_destroy", ctypes.c_int, [ctypes.c_void_p])
 _HANDLES: dict[tuple[int, str], torch.cuda.ExternalStream] = {}
 
@@ -80,3 +93,57 @@ def side_stream(device: torch.device, role: str, owner=None) -> torch.cuda.Strea
     else:
         weakref.finalize(owner, _destroy, h.value, idx)
     return st
+
+
+def reserve_compute_queue(device: torch.device | int | None = None, candidates: int = 128) -> int:
+    """Keep later streams off the compute (null) stream's hardware queue (see the module docstring); once per device
+    and process, before anything else creates streams.  Returns the number of blocker streams kept (0 when disabled
+    with ``DLLM_QUEUE_RESERVE=0``)."""
+    if os.environ.get("DLLM_QUEUE_RESERVE", "1") == "0":
+        return 0
+    idx = _index(device)
+    if idx not in _RESERVED:
+        with torch.cuda.device(idx):
+            n = _native.lib().dllm_queue_reserve(None, int(candidates), PROBE_SPIN_US)
+        if n < 0:
+            raise RuntimeError(f"dllm_queue_reserve failed ({n})")
+        _RESERVED[idx] = n
+    return _RESERVED[idx]
+
+
+def _index(device) -> int:
+    if device is None:
+        return torch.cuda.current_device()
+    if isinstance(device, int):
+        return device
+    return device.index if device.index is not None else torch.cuda.current_device()
+
+
+def shares_compute_queue(stream: torch.cuda.Stream, device=None) -> bool:
+    """Whether ``stream`` runs on the compute (null) stream's hardware queue (measured; synchronises both)."""
+    with torch.cuda.device(_index(device)):
+        r = _native.lib().dllm_queue_shared(None, ctypes.c_void_p(stream.cuda_stream), PROBE_SPIN_US)
+    if r < 0:
+        raise RuntimeError(f"dllm_queue_shared failed ({r})")
+    return r == 1
+
+
+def queue_report(device, streams: dict, pool: bool = True) -> dict:
+    """Which of ``streams`` ({name: stream}, None entries skipped) -- plus, with ``pool``, torch's 32 normal-priority
+    pool streams, which ProcessGroupNCCL's collective streams come from -- share the compute stream's hardware queue.
+    Idle GPU expected (each probe synchronises)."""
+    idx = _index(device)
+    shared = [n for n, st in streams.items() if st is not None and st.cuda_stream != 0 and shares_compute_queue(st, idx)]
+    npool = 0
+    if pool:
+        seen = set()
+        for _ in range(32):
+            st = torch.cuda.Stream(device=idx)
+            if st.cuda_stream in seen:
+                continue
+            seen.add(st.cuda_stream)
+            npool += shares_compute_queue(st, idx)
+    return {"reserved_blockers": _RESERVED.get(idx, 0), "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES",
+                                                                                            "hip default"),
+            "side_streams_on_compute_queue": shared, "pool_streams_on_compute_queue": npool,
+            "compute_queue_exclusive": not shared and npool == 0}
