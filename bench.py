@@ -291,7 +291,8 @@ def run_method(a, method: str, n: int, world: int, dev: torch.device, steps: int
                       side_optimizer=a.side_opt if headline else 0, tp_allreduce=a.tp_allreduce,
                       relu_mask=not a.no_relu_mask, gemm_tiles_per_block=a.tpb, fp32_gemm=a.fp32_gemm,
                       gemm_min_bpc=a.min_bpc, master=a.master, wgrad_stream_max_tpc=a.wgrad_stream_max_tpc,
-                      wgrad_stream=a.wgrad_stream and headline and not a.graph)
+                      wgrad_stream=a.wgrad_stream and headline and not a.graph,
+                      tp_transposed=os.environ.get("DLLM_TP_TRANSPOSED", "1") != "0")
     mesh = Mesh.build(dp, tp, force=force_comm, comm_backend="torch" if cpu else a.comm,
                       device=None if cpu else dev)
     try:

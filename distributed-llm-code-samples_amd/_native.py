@@ -23,7 +23,7 @@ _ERR: str | None = None
 c_int, c_long, c_float, c_void_p, c_ull = ctypes.c_int, ctypes.c_long, ctypes.c_float, ctypes.c_void_p, ctypes.c_ulonglong
 
 # bumped with every signature change below (csrc/elementwise.hip dllm_abi_version): a stale library fails loudly
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 _SIGS = {
     "dllm_gemm": (c_int, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_long, c_void_p, c_long, c_void_p, c_long,
@@ -33,7 +33,7 @@ _SIGS = {
     "dllm_gemm_path": (c_int, [c_int, c_int, c_int, c_int, c_int, c_long, c_long, c_long]),
     "dllm_queue_shared": (c_int, [c_void_p, c_void_p, c_int]),
     "dllm_queue_reserve": (c_int, [c_void_p, c_int, c_int]),
-    "dllm_gemm_pair": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+    "dllm_gemm_pair": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_float, c_float, c_float,
                                c_float, c_float, c_float, c_int, c_void_p]),
     "dllm_rng_normal": (c_int, [c_void_p, c_int, c_long, c_ull, c_ull, c_float, c_void_p]),

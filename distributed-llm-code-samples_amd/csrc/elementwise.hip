@@ -31,14 +31,15 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
   return c;
 }
 
+// Box-Muller on the hardware transcendentals: v_log_f32 is log2 (so -2 ln u1 = -2 ln2 * log2 u1), v_sqrt_f32, and
+// v_sin_f32 / v_cos_f32 take their argument in revolutions -- u2 in [0, 1) is already one, so no 2*pi scaling and no
+// range reduction (the libm-style __sincosf path reduced the argument first).
 __device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, float& z0, float& z1) {
   const float u1 = ((float)a + 1.0f) * 2.3283064365386963e-10f;  // (0, 1]
-  const float u2 = (float)b * 2.3283064365386963e-10f;           // [0, 1)
-  const float r = __builtin_amdgcn_sqrtf(-2.0f * __logf(u1));  // v_sqrt_f32 (1 ulp; no IEEE fix-up sequence)
-  float s, c;
-  __sincosf(6.283185307179586f * u2, &s, &c);
-  z0 = r * c;
-  z1 = r * s;
+  const float u2 = (float)b * 2.3283064365386963e-10f;           // [0, 1) revolutions
+  const float r = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));
+  z0 = r * __builtin_amdgcn_cosf(u2);
+  z1 = r * __builtin_amdgcn_sinf(u2);
 }
 
 template <typename OutT>
@@ -477,10 +478,10 @@ int dllm_queue_reserve(void* base, int candidates, int spin_us) {
     }
   }
   for (int i = 0; i < made; ++i)
-    if (cand[i]) hipStreamDestroy(cand[i]);
+    if (cand[i]) (void)hipStreamDestroy(cand[i]);
   return nblock;
 }
 
-int dllm_abi_version() { return 9; }
+int dllm_abi_version() { return 10; }
 
 }  // extern "C"

@@ -20,7 +20,7 @@ static int pp_skew() {
 extern "C" {
 
 // Returns 0 on success, a hipError_t otherwise, or -1 for a bad argument.
-// force_path: -1 auto, 0 bf16-256 tile kernel, 1 fp32-128 kernel, 2 generic kernel.
+// force_path: -1 auto, 0 bf16-256 tile kernel, 1 fp32-128 kernel, 2 generic kernel, 3 bf16 224-row tiles.
 int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const void* A, long lda,
               const void* B, long ldb, void* C, long ldc, const void* aux, void* aux_out, long ldaux,
               int M, int N, int K, float alpha, float beta, int group_m, int force_path, void* stream,
@@ -50,7 +50,7 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
                            ((uintptr_t)opt_m % 16 == 0) && ((uintptr_t)opt_v % 16 == 0);
   const bool opt_epi = (epi == EPI_SGD || epi == EPI_ADAM || epi == EPI_SGDS || epi == EPI_ADAMS);
   const bool split_epi = (epi == EPI_SGDS || epi == EPI_ADAMS);
-  if (opt_epi && layout != L_TN) return -1;
+  if (opt_epi && layout == L_NT) return -1;
   if ((epi == EPI_SGD || epi == EPI_ADAM) && out_dtype != DT_F32) return -1;
   // split master: C = the 16-bit residual plane, aux_out = the bf16 working copy (paired 16-B rows: ld % 8 == 0)
   if (split_epi && (out_dtype != DT_BF16 || in_dtype != DT_BF16 || aux_out == nullptr)) return -1;
@@ -64,11 +64,17 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
                            (!split_epi || (ldc % 8 == 0 && ldaux % 8 == 0));
   if (in_dtype == DT_BF16 && M % BT_M == 0 && N % BT_N == 0 && K % BT_K == 0 && aligned_lds) path = 0;
   if (in_dtype == DT_F32 && out_dtype == DT_F32 && M % FT == 0 && N % FT == 0 && K % FK == 0 && aligned_lds) path = 1;
+  // 224-row tiles: M = 224 * k but not 256-tiled (the MP / TP8 shard's F/8 rows), K-contiguous A, 8-phase K step
+  if (in_dtype == DT_BF16 && M % BT_M != 0 && M % 224 == 0 && N % BT_N == 0 && K % (2 * BT_K) == 0 && aligned_lds &&
+      layout != L_TN && epi != EPI_GLU && epi != EPI_DGLU && ksplit <= 1 && variant != 5)
+    path = 3;
   if (force_path >= 0) {
     if (force_path == 0 && path != 0) return -1;
     if (force_path == 1 && path != 1) return -1;
+    if (force_path == 3 && path != 3) return -1;
     path = force_path;
   }
+  if (opt_epi && layout == L_NN && path != 3) return -1;  // NN fused optimizers: 224-row tiles only
   if (path == 2 && epi == EPI_GLU && aux_out == nullptr) return -1;
   if (ksplit > 1) {
     // split-K only on the bf16 8-phase path (each slice an even number of 64-deep K-tiles); a request
@@ -82,14 +88,14 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
   if (mask != nullptr) {
     // the bitmask lives in the 8-phase kernels' tile-native layout: both GEMMs of a pair must run them
     if ((epi != EPI_ACT && epi != EPI_DACT) || act != ACT_RELU || in_dtype != DT_BF16 || out_dtype != DT_BF16 ||
-        path != 0 || a.ksplit != 1 || (K % (2 * BT_K) != 0 && a.variant != 5) || a.variant == 1)
+        (path != 0 && path != 3) || a.ksplit != 1 || (K % (2 * BT_K) != 0 && a.variant != 5) || a.variant == 1)
       return -2;
     a.mask = mask;
   }
   hipStream_t s = (hipStream_t)stream;
   hipError_t e;
   if (opt_epi) {
-    e = dispatch_tn_opt(path, epi, a, in_dtype, s);
+    e = (layout == L_NN && path == 3) ? dispatch_nn_opt(epi, a, s) : dispatch_tn_opt(path, epi, a, in_dtype, s);
     return (int)e;
   }
   switch (layout) {
@@ -111,15 +117,19 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
   return (int)e;
 }
 
-// Two TN (weight-gradient) GEMMs of one epilogue and one K in a single grouped launch, one 256x256 tile per block
-// (gemm_bf16_8ph_pair).  Per-problem arrays of 2: A, lda, B, ldb, C, ldc, aux_out, ldaux, opt_m, opt_v, M, N.  Returns
-// -1 when the pair does not fit the grouped kernel (the caller then runs two dllm_gemm calls): bf16 operands, both
-// shapes 256-tiled, K % 128 == 0, 16-B aligned, and tiles(0) + tiles(1) <= the device's CUs.
-int dllm_gemm_pair(int out_dtype, int epi, const void* const* A, const long* lda, const void* const* B,
+// Two weight-gradient GEMMs of one layout, epilogue and K in a single grouped launch, one tile per block
+// (gemm_bf16_8ph_pair): TN on 256x256 tiles, or NN on 224x256 tiles (the transposed-activation TP layout).  Per-problem
+// arrays of 2: A, lda, B, ldb, C, ldc, aux_out, ldaux, opt_m, opt_v, M, N.  Returns -1 when the pair does not fit the
+// grouped kernel (the caller then runs two dllm_gemm calls): bf16 operands, both shapes tiled, K % 128 == 0, 16-B
+// aligned, and tiles(0) + tiles(1) <= the device's CUs.
+int dllm_gemm_pair(int layout, int out_dtype, int epi, const void* const* A, const long* lda, const void* const* B,
                    const long* ldb, void* const* C, const long* ldc, void* const* aux_out, const long* ldaux,
                    float* const* opt_m, float* const* opt_v, const int* M, const int* N, int K, float alpha,
                    float lr, float b1, float b2, float eps, float wd, int step, void* stream) {
   if (K <= 0 || K % (2 * BT_K) != 0) return -1;
+  if (layout != L_TN && layout != L_NN) return -1;
+  // TN: 256-row tiles; NN: 224-row tiles (the transposed-activation TP layout's dW2ᵀ / dW1, M = F/tp)
+  const int bm = layout == L_TN ? BT_M : 224;
   if (epi != EPI_STORE && epi != EPI_SGD && epi != EPI_SGDS && epi != EPI_ADAM && epi != EPI_ADAMS) return -1;
   const bool split_epi = (epi == EPI_SGDS || epi == EPI_ADAMS);
   if ((epi == EPI_SGD || epi == EPI_ADAM) && out_dtype != DT_F32) return -1;
@@ -127,7 +137,7 @@ int dllm_gemm_pair(int out_dtype, int epi, const void* const* A, const long* lda
   GemmArgs a[2];
   int tiles = 0;
   for (int i = 0; i < 2; ++i) {
-    if (M[i] <= 0 || N[i] <= 0 || M[i] % BT_M || N[i] % BT_N) return -1;
+    if (M[i] <= 0 || N[i] <= 0 || M[i] % bm || N[i] % BT_N) return -1;
     if (split_epi && aux_out[i] == nullptr) return -1;
     if ((epi == EPI_ADAM || epi == EPI_ADAMS) && (step < 1 || !opt_m[i] || !opt_v[i])) return -1;
     const bool al = ((uintptr_t)A[i] % 16 == 0) && ((uintptr_t)B[i] % 16 == 0) && ((uintptr_t)C[i] % 16 == 0) &&
@@ -148,17 +158,19 @@ int dllm_gemm_pair(int out_dtype, int epi, const void* const* A, const long* lda
     }
     g.ksplit = 1; g.tpb = 1; g.variant = 3; g.tpb_req = 1; g.min_bpc = 1; g.ws = nullptr; g.mask = nullptr;
     g.skew = 0;
-    tiles += (M[i] / BT_M) * (N[i] / BT_N);
+    tiles += (M[i] / bm) * (N[i] / BT_N);
   }
   const int ncu = num_cu();
   if (ncu <= 0 || tiles > ncu) return -1;
-  return (int)dispatch_tn_pair(epi, a[0], a[1], out_dtype, (hipStream_t)stream);
+  return (int)(layout == L_TN ? dispatch_tn_pair(epi, a[0], a[1], out_dtype, (hipStream_t)stream)
+                              : dispatch_nn_pair(epi, a[0], a[1], out_dtype, (hipStream_t)stream));
 }
 
-// which kernel family dllm_gemm would pick (for tests / profiling labels)
+// which kernel family dllm_gemm would pick (for tests / profiling labels; 224-row tiles need a K-contiguous A too)
 int dllm_gemm_path(int in_dtype, int out_dtype, int M, int N, int K, long lda, long ldb, long ldc) {
   const bool al = (lda % 8 == 0) && (ldb % 8 == 0) && (ldc % 4 == 0);  // (bases: checked per call)
   if (in_dtype == DT_BF16 && M % BT_M == 0 && N % BT_N == 0 && K % BT_K == 0 && al) return 0;
+  if (in_dtype == DT_BF16 && M % 224 == 0 && N % BT_N == 0 && K % (2 * BT_K) == 0 && al) return 3;
   if (in_dtype == DT_F32 && out_dtype == DT_F32 && M % FT == 0 && N % FT == 0 && K % FK == 0 && al) return 1;
   return 2;
 }

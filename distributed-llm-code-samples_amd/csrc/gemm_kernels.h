@@ -292,9 +292,12 @@ __device__ __forceinline__ void unpair_bf16(uint4 v, f32x4_t& a, f32x4_t& b) {
 // acc[QM][QN][mt][nt]: lane holds C[m0 + QM*128 + wr*64 + mt*16 + (lane&15)][n0 + QN*QNS + wc*32 + nt*16 + 4*(lane>>4) + 0..3]
 // row group rg = QM*8 + QN*4 + mt (16 per wave), 2 column groups (nt) each.  QNS = quadrant width: 128 for the
 // 256x256 tile (8 waves, wc 0..3), 64 for the 256x128 tile of gemm_bf16_pp (4 waves, wc 0..1).
-template <int EPI, typename OutT, int ACT, int QNS = 128>
+// BM = 224 (gemm_8ph_body): the second row half has 3 row fragments per wave, at rows 128 + wr*48 + mt*16; row
+// groups with QM = 1, mt = 3 do not exist (DLLM_OK).
+template <int EPI, typename OutT, int ACT, int QNS = 128, int BM = 256>
 __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2][2][4][2], int m0, int n0,
                                              int wr, int wc, int lane, void* Cp) {
+  static_assert(BM == 256 || (QNS == 128 && EPI != EPI_GLU && EPI != EPI_DGLU), "224-row tiles: no gated epilogues");
   constexpr int NWC = QNS / 32;       // waves per tile row
   constexpr int TW = 2 * QNS;         // tile width
   constexpr int MASK_WAVES = 2 * NWC; // waves per tile: the ReLU mask holds 16 B per lane and wave
@@ -309,7 +312,8 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
                      : EPI == EPI_SGD || EPI == EPI_SGDS ? 8 : EPI == EPI_ADAM || EPI == EPI_ADAMS ? 24 : 0;
   constexpr int RB = epi_batch(COST);
   const int pc = pair_col(lane);
-#define DLLM_M(rg) (m0 + ((rg) >> 3) * 128 + wr * 64 + ((rg) & 3) * 16 + (lane & 15))
+#define DLLM_M(rg) (m0 + ((rg) >> 3) * 128 + wr * ((BM != 256 && ((rg) >> 3)) ? 48 : 64) + ((rg) & 3) * 16 + (lane & 15))
+#define DLLM_OK(rg) (BM == 256 || ((rg) >> 3) == 0 || ((rg) & 3) != 3)
 #define DLLM_NB(rg) (n0 + (((rg) >> 2) & 1) * QNS + wc * 32)
 #define DLLM_N(rg, nt) (DLLM_NB(rg) + (nt) * 16 + 4 * (lane >> 4))
 #define DLLM_ACC(rg, nt) acc[(rg) >> 3][((rg) >> 2) & 1][(rg) & 3][nt]
@@ -339,15 +343,18 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
     if (p.beta == 0.f) {
 #pragma unroll
       for (int rg = 0; rg < 16; ++rg)
-        store_rg(Cp, p.ldc, DLLM_M(rg), DLLM_NB(rg), DLLM_ACC(rg, 0) * p.alpha, DLLM_ACC(rg, 1) * p.alpha);
+        if (DLLM_OK(rg))
+          store_rg(Cp, p.ldc, DLLM_M(rg), DLLM_NB(rg), DLLM_ACC(rg, 0) * p.alpha, DLLM_ACC(rg, 1) * p.alpha);
     } else {
 #pragma unroll
       for (int b0 = 0; b0 < 16; b0 += RB) {
         RT L[RB][2];
 #pragma unroll
-        for (int r = 0; r < RB; ++r) load_rg(Cp, p.ldc, DLLM_M(b0 + r), DLLM_NB(b0 + r), L[r]);
+        for (int r = 0; r < RB; ++r)
+          if (DLLM_OK(b0 + r)) load_rg(Cp, p.ldc, DLLM_M(b0 + r), DLLM_NB(b0 + r), L[r]);
 #pragma unroll
         for (int r = 0; r < RB; ++r) {
+          if (!DLLM_OK(b0 + r)) continue;
           f32x4_t c0, c1;
           decode_rg(L[r], c0, c1);
           store_rg(Cp, p.ldc, DLLM_M(b0 + r), DLLM_NB(b0 + r), DLLM_ACC(b0 + r, 0) * p.alpha + p.beta * c0,
@@ -359,17 +366,24 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
     if (p.aux_out) {
 #pragma unroll
       for (int rg = 0; rg < 16; ++rg)
-        store_rg(p.aux_out, p.ldaux, DLLM_M(rg), DLLM_NB(rg), DLLM_ACC(rg, 0), DLLM_ACC(rg, 1));
+        if (DLLM_OK(rg)) store_rg(p.aux_out, p.ldaux, DLLM_M(rg), DLLM_NB(rg), DLLM_ACC(rg, 0), DLLM_ACC(rg, 1));
     }
     if constexpr (ACT == ACT_RELU && BF) {
       // optional mask: bit rg*8 + nt*4 + e of this thread's 128 = (stored bf16 activation != 0), i.e. exactly
       // the act'(h) the unmasked dgrad derives from the stored activation; one dword per 4 row groups
       const bool mk = p.mask != nullptr;
-      const long tile = (long)(m0 / 256) * (p.N / TW) + n0 / TW;  // 256 x TW tiles
+      const long tile = (long)(m0 / BM) * (p.N / TW) + n0 / TW;  // BM x TW tiles
       uint32_t* mw = (uint32_t*)p.mask + (tile * (MASK_WAVES * 64) + (wr * NWC + wc) * 64 + lane) * 4;
       uint32_t w = 0u;
 #pragma unroll
       for (int rg = 0; rg < 16; ++rg) {
+        if (!DLLM_OK(rg)) {  // 224-row tile: no such row group; still flush its mask word
+          if (mk && (rg & 3) == 3) {
+            mw[rg >> 2] = w;
+            w = 0u;
+          }
+          continue;
+        }
         f32x4_t a = DLLM_ACC(rg, 0), b = DLLM_ACC(rg, 1);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -394,6 +408,7 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
     }
 #pragma unroll
     for (int rg = 0; rg < 16; ++rg) {
+      if (!DLLM_OK(rg)) continue;
       f32x4_t a = DLLM_ACC(rg, 0), b = DLLM_ACC(rg, 1);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -405,11 +420,12 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
   } else if constexpr (EPI == EPI_DACT) {
     if constexpr (ACT == ACT_RELU && BF) {
       if (p.mask) {
-        const long tile = (long)(m0 / 256) * (p.N / TW) + n0 / TW;  // 256 x TW tiles
+        const long tile = (long)(m0 / BM) * (p.N / TW) + n0 / TW;  // BM x TW tiles
         const uint4 mv = ((const uint4*)p.mask)[tile * (MASK_WAVES * 64) + (wr * NWC + wc) * 64 + lane];
         const uint32_t w[4] = {mv.x, mv.y, mv.z, mv.w};
 #pragma unroll
         for (int rg = 0; rg < 16; ++rg) {
+          if (!DLLM_OK(rg)) continue;
           const uint32_t bits = w[rg >> 2] >> ((rg & 3) * 8);
           f32x4_t a = DLLM_ACC(rg, 0), b = DLLM_ACC(rg, 1);
 #pragma unroll
@@ -426,9 +442,11 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
     for (int b0 = 0; b0 < 16; b0 += RB) {
       RT H[RB][2];
 #pragma unroll
-      for (int r = 0; r < RB; ++r) load_rg(p.aux, p.ldaux, DLLM_M(b0 + r), DLLM_NB(b0 + r), H[r]);
+      for (int r = 0; r < RB; ++r)
+        if (DLLM_OK(b0 + r)) load_rg(p.aux, p.ldaux, DLLM_M(b0 + r), DLLM_NB(b0 + r), H[r]);
 #pragma unroll
       for (int r = 0; r < RB; ++r) {
+        if (!DLLM_OK(b0 + r)) continue;
         f32x4_t h0, h1;
         decode_rg(H[r], h0, h1);
         f32x4_t a = DLLM_ACC(b0 + r, 0), b = DLLM_ACC(b0 + r, 1);
@@ -524,11 +542,13 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
 #pragma unroll
       for (int r = 0; r < RB; ++r)
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) W[r][nt] = RF::load(Cp, (long)DLLM_M(b0 + r) * p.ldc + DLLM_N(b0 + r, nt));
+        for (int nt = 0; nt < 2; ++nt)
+          if (DLLM_OK(b0 + r)) W[r][nt] = RF::load(Cp, (long)DLLM_M(b0 + r) * p.ldc + DLLM_N(b0 + r, nt));
 #pragma unroll
       for (int r = 0; r < RB; ++r)
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) {
+          if (!DLLM_OK(b0 + r)) continue;
           const f32x4_t g = DLLM_ACC(b0 + r, nt);
 #pragma unroll
           for (int e = 0; e < 4; ++e)
@@ -538,7 +558,8 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
       if (p.aux_out) {
 #pragma unroll
         for (int r = 0; r < RB; ++r)
-          st_pair_bf16(p.aux_out, (long)DLLM_M(b0 + r) * p.ldaux + DLLM_NB(b0 + r) + pc, W[r][0], W[r][1]);
+          if (DLLM_OK(b0 + r))
+            st_pair_bf16(p.aux_out, (long)DLLM_M(b0 + r) * p.ldaux + DLLM_NB(b0 + r) + pc, W[r][0], W[r][1]);
       }
     }
   } else if constexpr (EPI == EPI_SGDS) {
@@ -550,11 +571,13 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
       uint4 H[RB], Lw[RB];
 #pragma unroll
       for (int r = 0; r < RB; ++r) {
+        if (!DLLM_OK(b0 + r)) continue;
         H[r] = *(const uint4*)((const uint16_t*)p.aux_out + (long)DLLM_M(b0 + r) * p.ldaux + DLLM_NB(b0 + r) + pc);
         Lw[r] = *(const uint4*)((const uint16_t*)Cp + (long)DLLM_M(b0 + r) * p.ldc + DLLM_NB(b0 + r) + pc);
       }
 #pragma unroll
       for (int r = 0; r < RB; ++r) {
+        if (!DLLM_OK(b0 + r)) continue;
         // after the exchange: words 0-1 hold the nt = 0 fragment's 4 columns, words 2-3 the nt = 1 fragment's
         const uint4 h = pair_swap(uint2{H[r].x, H[r].y}, uint2{H[r].z, H[r].w});
         const uint4 l = pair_swap(uint2{Lw[r].x, Lw[r].y}, uint2{Lw[r].z, Lw[r].w});
@@ -584,6 +607,7 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
       f32x4_t Mm[RB][2], Vv[RB][2];
 #pragma unroll
       for (int r = 0; r < RB; ++r) {
+        if (!DLLM_OK(b0 + r)) continue;
         H[r] = *(const uint4*)((const uint16_t*)p.aux_out + (long)DLLM_M(b0 + r) * p.ldaux + DLLM_NB(b0 + r) + pc);
         Lw[r] = *(const uint4*)((const uint16_t*)Cp + (long)DLLM_M(b0 + r) * p.ldc + DLLM_NB(b0 + r) + pc);
 #pragma unroll
@@ -595,6 +619,7 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
       }
 #pragma unroll
       for (int r = 0; r < RB; ++r) {
+        if (!DLLM_OK(b0 + r)) continue;
         const uint4 h = pair_swap(uint2{H[r].x, H[r].y}, uint2{H[r].z, H[r].w});
         const uint4 l = pair_swap(uint2{Lw[r].x, Lw[r].y}, uint2{Lw[r].z, Lw[r].w});
         uint32_t hw[4] = {h.x, h.y, h.z, h.w}, lw[4] = {l.x, l.y, l.z, l.w};
@@ -635,6 +660,7 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
       for (int r = 0; r < SB; ++r)
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) {
+          if (!DLLM_OK(b * SB + r)) continue;
           const long ci = (long)DLLM_M(b * SB + r) * p.ldc + DLLM_N(b * SB + r, nt);
           W[s][r][nt] = RF::load(Cp, ci);
           Mm[s][r][nt] = RF::load(p.opt_m, ci);
@@ -648,6 +674,7 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
       const int s = b & 1;
 #pragma unroll
       for (int r = 0; r < SB; ++r) {
+        if (!DLLM_OK(b * SB + r)) continue;
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) {
           const f32x4_t gg = DLLM_ACC(b * SB + r, nt);
@@ -677,6 +704,7 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
       for (int r = 0; r < RB; ++r)
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) {
+          if (!DLLM_OK(b0 + r)) continue;
           const long ci = (long)DLLM_M(b0 + r) * p.ldc + DLLM_N(b0 + r, nt);
           W[r][nt] = RF::load(Cp, ci);
           Mm[r][nt] = RF::load(p.opt_m, ci);
@@ -686,6 +714,7 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
       for (int r = 0; r < RB; ++r)
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) {
+          if (!DLLM_OK(b0 + r)) continue;
           const f32x4_t gg = DLLM_ACC(b0 + r, nt);
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
@@ -703,11 +732,13 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
       if (p.aux_out) {
 #pragma unroll
         for (int r = 0; r < RB; ++r)
-          st_pair_bf16(p.aux_out, (long)DLLM_M(b0 + r) * p.ldaux + DLLM_NB(b0 + r) + pc, W[r][0], W[r][1]);
+          if (DLLM_OK(b0 + r))
+            st_pair_bf16(p.aux_out, (long)DLLM_M(b0 + r) * p.ldaux + DLLM_NB(b0 + r) + pc, W[r][0], W[r][1]);
       }
     }
   }
 #undef DLLM_M
+#undef DLLM_OK
 #undef DLLM_NB
 #undef DLLM_N
 #undef DLLM_ACC
@@ -975,8 +1006,13 @@ __device__ __forceinline__ GemmArgs reload_args(int which = 0) {
 // halves the barrier count per MFMA (see the NPH == 4 loop).
 // GRP: one block of a grouped launch (gemm_bf16_8ph_pair): ``p`` is argument block ``which`` of the kernel, ``slot0``
 // the block's tile in that problem (already XCD-remapped over the whole grid); one tile per block.
-template <int LAYOUT, int EPI, typename OutT, bool STAGGER, int ACT, int NPH, bool PERS, bool GRP>
+// BM = 224: 224-row tiles (A half-tiles of 128 + 96 rows; each wave row 64 + 48 rows, i.e. 4 + 3 row fragments), for
+// GEMMs whose M is a multiple of 224 but not of 256 -- the MP (TP8) shard's F/8 = 1792 = 8 x 224 rows, which a 256-row
+// tile grid fills only 7/8 of (224 tiles on 256 CUs).  K-contiguous A only (NT / NN), one tile per block.
+template <int LAYOUT, int EPI, typename OutT, bool STAGGER, int ACT, int NPH, bool PERS, bool GRP, int BM = BT_M>
 __device__ __forceinline__ void gemm_8ph_body(const GemmArgs& p, const int which, const int slot0) {
+  static_assert(BM == BT_M || (BM == 224 && LAYOUT != L_TN && NPH == 8 && !PERS), "224-row tiles: K-contiguous A, 8 phases");
+  constexpr int MT1 = BM == BT_M ? 4 : 3;  // row fragments per wave in the second A half
   // slot(op, hh, buf) = ((op*2 + hh)*2 + buf) * 16 KiB: A in [0, 64K), B in [64K, 128K), so every
   // fragment read is base + a 16-bit immediate
   __shared__ __attribute__((aligned(16))) char smem[8 * HT];
@@ -984,7 +1020,7 @@ __device__ __forceinline__ void gemm_8ph_body(const GemmArgs& p, const int which
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wid >> 2, wc = wid & 3;
-  const int tiles_m = p.M / BT_M, tiles_n = p.N / BT_N;
+  const int tiles_m = p.M / BM, tiles_n = p.N / BT_N;
   const int ntiles = tiles_m * tiles_n;
   const int total = ntiles * p.ksplit;  // tile slots (split-K slices count as tiles)
   // Persistent blocks (PERS, NPH == 8, p.tpb > 1): block b runs slots b, b + G, b + 2G, ... (G = gridDim.x,
@@ -997,14 +1033,14 @@ __device__ __forceinline__ void gemm_8ph_body(const GemmArgs& p, const int which
   // reload_args() copy, so the epilogue's arguments are loaded where they are used instead of being kept
   // live in SGPRs across the whole main loop.
   auto tile_of = [&](const GemmArgs& q, int s, int& sp, int& tm0, int& tn0) {
-    const int tm_ = q.M / BT_M, tn_ = q.N / BT_N, nt = tm_ * tn_;
+    const int tm_ = q.M / BM, tn_ = q.N / BT_N, nt = tm_ * tn_;
     const int bid0 = GRP ? s : xcd_remap(s, pers ? nt * q.ksplit : (int)gridDim.x);
     sp = bid0 / nt;  // split-K slice (0 when ksplit == 1)
     const int bid = bid0 % nt;
     const int width = q.group_m * tn_;
     const int first_m = (bid / width) * q.group_m;
     const int gsz = min(tm_ - first_m, q.group_m);
-    tm0 = (first_m + (bid % width) % gsz) * BT_M;
+    tm0 = (first_m + (bid % width) % gsz) * BM;
     tn0 = ((bid % width) / gsz) * BT_N;
   };
   constexpr bool A_KC = (LAYOUT != L_TN);
@@ -1013,6 +1049,16 @@ __device__ __forceinline__ void gemm_8ph_body(const GemmArgs& p, const int which
   constexpr bool B_RKC = B_KC;
   uint32_t aoff[2], boff[2];
   if constexpr (A_KC) kc_half_offsets(p.lda, wid, lane, aoff); else mc_half_offsets(p.lda, wid, lane, aoff);
+  // BM = 224: the second A half has 96 rows; the DMA pieces of rows 96..127 re-load row 95 (slots never read), so
+  // every wave still issues the same loads and the counted waits stay static
+  uint32_t aoff1[2] = {aoff[0], aoff[1]};
+  if constexpr (BM != BT_M) {
+    const int row = 8 * (wid + 8) + (lane >> 3);  // piece wid + 8 (the only ones that can pass row 95)
+    if (row >= BM - 128) {
+      const int r = BM - 128 - 1, c = (lane & 7) ^ ((r >> 1) & 7);
+      aoff1[1] = (uint32_t)(((long)r * p.lda + c * 8) * 2);
+    }
+  }
   if constexpr (B_KC) kc_half_offsets(p.ldb, wid, lane, boff); else mc_half_offsets(p.ldb, wid, lane, boff);
   const long a_kstep = A_KC ? BT_K : (long)BT_K * p.lda;
   const long b_kstep = B_KC ? BT_K : (long)BT_K * p.ldb;
@@ -1038,7 +1084,7 @@ __device__ __forceinline__ void gemm_8ph_body(const GemmArgs& p, const int which
     void* out = q.C;
     if constexpr (EPI == EPI_STORE)
       if (q.ksplit > 1) out = (char*)q.C + (long)sp * q.M * q.ldc * sizeof(OutT);
-    epilogue_256<EPI, OutT, ACT>(q, ac, tm0, tn0, wr, wc, lane, out);
+    epilogue_256<EPI, OutT, ACT, 128, BM>(q, ac, tm0, tn0, wr, wc, lane, out);
   };
   // next slot of this block (>= total: none)
   int next_slot = total;
@@ -1049,7 +1095,7 @@ __device__ __forceinline__ void gemm_8ph_body(const GemmArgs& p, const int which
   auto stage_at = [&](int op, int hh, const uint16_t* src, int buf) {
     DLLM_LDS char* dst = lds + ((op * 2 + hh) * 2 + buf) * HT;
     src += op == 0 ? hh * a_hstep : hh * b_hstep;
-    const uint32_t* off = op == 0 ? aoff : boff;
+    const uint32_t* off = op == 0 ? (hh == 1 ? aoff1 : aoff) : boff;
     glds16((const uint16_t*)((const char*)src + off[0]), dst + wid * 1024);
     glds16((const uint16_t*)((const char*)src + off[1]), dst + (wid + 8) * 1024);
   };
@@ -1073,10 +1119,14 @@ __device__ __forceinline__ void gemm_8ph_body(const GemmArgs& p, const int which
   const int fkc = (i15 >> 1) & 7;
   // MN-contiguous image (256-B rows, unit ^= (k&3)|((k>>3)&1)<<2): per tile t
   const int q = i15 >> 2, pp = i15 & 3, swz = q | ((g & 1) << 2);
-  uint32_t abase[4], bbase[2];
+  uint32_t abase[4], bbase[2], abase1[2];
   if constexpr (A_RKC) {
     abase[0] = lds_base + (wr * 64 + i15) * 128 + (((0 + g) ^ fkc) << 4);
     abase[1] = lds_base + (wr * 64 + i15) * 128 + (((4 + g) ^ fkc) << 4);
+    // second A half of a 224-row tile: wave row wr reads rows wr*48 + mt*16 (the chunk swizzle depends on row bits
+    // 1-3 only, which 48*wr does not touch)
+    abase1[0] = abase[0] - (BM == BT_M ? 0 : wr * 16 * 128);
+    abase1[1] = abase[1] - (BM == BT_M ? 0 : wr * 16 * 128);
   } else {
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -1108,7 +1158,12 @@ __device__ __forceinline__ void gemm_8ph_body(const GemmArgs& p, const int which
   // A half hh of buffer buf -> fa ; B half hh of buffer buf -> fb   (issue only)
   auto read_a = [&](auto hh_c, auto buf_c) {
     constexpr int SO = (hh_c.value * 2 + buf_c.value) * HT;
-    if constexpr (A_RKC) {
+    if constexpr (A_RKC && BM != BT_M && hh_c.value == 1) {
+      lds_b128<SO + 0 * 2048>(fa[0][0], abase1[0]); lds_b128<SO + 1 * 2048>(fa[1][0], abase1[0]);
+      lds_b128<SO + 2 * 2048>(fa[2][0], abase1[0]);
+      lds_b128<SO + 0 * 2048>(fa[0][1], abase1[1]); lds_b128<SO + 1 * 2048>(fa[1][1], abase1[1]);
+      lds_b128<SO + 2 * 2048>(fa[2][1], abase1[1]);
+    } else if constexpr (A_RKC) {
       lds_b128<SO + 0 * 2048>(fa[0][0], abase[0]); lds_b128<SO + 1 * 2048>(fa[1][0], abase[0]);
       lds_b128<SO + 2 * 2048>(fa[2][0], abase[0]); lds_b128<SO + 3 * 2048>(fa[3][0], abase[0]);
       lds_b128<SO + 0 * 2048>(fa[0][1], abase[1]); lds_b128<SO + 1 * 2048>(fa[1][1], abase[1]);
@@ -1171,14 +1226,16 @@ __device__ __forceinline__ void gemm_8ph_body(const GemmArgs& p, const int which
         for (int s2 = 0; s2 < 2; ++s2) fb[t][s2] = cat_tr(tc_lo[t][s2], tc_hi[t][s2]);
     }
   };
-  auto mfma_quad = [&](f32x4_t (&c)[4][2], const bf16x8_t (&fb)[2][2]) {
+  // qm_c: the quadrant's A half (second half of a 224-row tile: MT1 row fragments)
+  auto mfma_quad = [&](f32x4_t (&c)[4][2], const bf16x8_t (&fb)[2][2], auto qm_c) {
+    constexpr int NMT = qm_c.value == 1 ? MT1 : 4;
 #if DLLM_PRIO_MODE == 0
     __builtin_amdgcn_s_setprio(1);
 #endif
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
+      for (int mt = 0; mt < NMT; ++mt)
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt)
           c[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[nt][s2], fa[mt][s2], c[mt][nt], 0, 0, 0);
@@ -1219,25 +1276,25 @@ __device__ __forceinline__ void gemm_8ph_body(const GemmArgs& p, const int which
       stage(1, 1, to, 1); stage(0, 1, to, 1);            // P0: B1 A1 odd
       DLLM_PHASE_END4(8)
       fin_a(); fin_b(fb0); fin_b2(fb1);
-      mfma_quad(acc[0][0], fb0); mfma_quad(acc[0][1], fb1);
+      mfma_quad(acc[0][0], fb0, I0{}); mfma_quad(acc[0][1], fb1, I0{});
       DLLM_BARRIER();
       read_a(I1{}, I0{});
       stage(0, 0, te + 2, 0); stage(1, 0, te + 2, 0);    // P1: A0 B0 even
       DLLM_PHASE_END4(6)
       fin_a();
-      mfma_quad(acc[1][1], fb1); mfma_quad(acc[1][0], fb0);
+      mfma_quad(acc[1][1], fb1, I1{}); mfma_quad(acc[1][0], fb0, I1{});
       DLLM_BARRIER();
       read_a(I0{}, I1{}); read_b(I0{}, I1{}, fb0); read_b2(I1{}, I1{}, fb1);
       stage(1, 1, te + 2, 0); stage(0, 1, te + 2, 0);    // P2: B1 A1 even
       DLLM_PHASE_END4(8)
       fin_a(); fin_b(fb0); fin_b2(fb1);
-      mfma_quad(acc[0][0], fb0); mfma_quad(acc[0][1], fb1);
+      mfma_quad(acc[0][0], fb0, I0{}); mfma_quad(acc[0][1], fb1, I0{});
       DLLM_BARRIER();
       read_a(I1{}, I1{});
       stage(0, 0, to + 2, 1); stage(1, 0, to + 2, 1);    // P3: A0 B0 odd
       DLLM_PHASE_END4(6)
       fin_a();
-      mfma_quad(acc[1][1], fb1); mfma_quad(acc[1][0], fb0);
+      mfma_quad(acc[1][1], fb1, I1{}); mfma_quad(acc[1][0], fb0, I1{});
       DLLM_BARRIER();
 #undef DLLM_PHASE_END4
     }
@@ -1275,46 +1332,46 @@ __device__ __forceinline__ void gemm_8ph_body(const GemmArgs& p, const int which
     }
     DLLM_PHASE_END(false)
     fin_a(); fin_b(fb0);
-    mfma_quad(acc[0][0], fb0);
+    mfma_quad(acc[0][0], fb0, I0{});
     DLLM_BARRIER();
     read_b(I1{}, I0{}, fb1);
     stage_at(0, 0, Apf, 0);                    // P1: A0 even (K-tile 2it+2)
     DLLM_PHASE_END(false)
     fin_b(fb1);
-    mfma_quad(acc[0][1], fb1);
+    mfma_quad(acc[0][1], fb1, I0{});
     DLLM_BARRIER();
     read_a(I1{}, I0{});
     stage_at(1, 0, Bpf, 0);                    // P2: B0 even
     DLLM_PHASE_END(false)
     fin_a();
-    mfma_quad(acc[1][1], fb1);
+    mfma_quad(acc[1][1], fb1, I1{});
     DLLM_BARRIER();
     stage_at(1, 1, Bpf, 0);                    // P3: B1 even
     DLLM_PHASE_END(true)
-    mfma_quad(acc[1][0], fb0);
+    mfma_quad(acc[1][0], fb0, I1{});
     DLLM_BARRIER();
     // ---- odd buffer (K-tile 2it+1) ----
     read_a(I0{}, I1{}); read_b(I0{}, I1{}, fb0);
     stage_at(0, 1, Apf, 0);                    // P4: A1 even
     DLLM_PHASE_END(false)
     fin_a(); fin_b(fb0);
-    mfma_quad(acc[0][0], fb0);
+    mfma_quad(acc[0][0], fb0, I0{});
     DLLM_BARRIER();
     read_b(I1{}, I1{}, fb1);
     stage_at(0, 0, Apf + a_kstep, 1);          // P5: A0 odd (K-tile 2it+3)
     DLLM_PHASE_END(false)
     fin_b(fb1);
-    mfma_quad(acc[0][1], fb1);
+    mfma_quad(acc[0][1], fb1, I0{});
     DLLM_BARRIER();
     read_a(I1{}, I1{});
     stage_at(1, 0, Bpf + b_kstep, 1);          // P6: B0 odd
     DLLM_PHASE_END(false)
     fin_a();
-    mfma_quad(acc[1][1], fb1);
+    mfma_quad(acc[1][1], fb1, I1{});
     DLLM_BARRIER();
     stage_at(1, 1, Bpf + b_kstep, 1);          // P7: B1 odd
     DLLM_PHASE_END(true)
-    mfma_quad(acc[1][0], fb0);
+    mfma_quad(acc[1][0], fb0, I1{});
     DLLM_BARRIER();
     Apf += 2 * a_kstep;
     Bpf += 2 * b_kstep;
@@ -1356,12 +1413,18 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph(GemmArgs p) {
 // and dW1 [F/8, D], 112 tiles each at F = 14336 -- instead of split-K slices and a reduction pass per GEMM.  The
 // remapped block ids are split [0, tiles(p0)) | [tiles(p0), ...), so each problem's tiles fill whole XCDs of their own
 // (no operand panel is shared across the two problems) and keep the grouped raster inside the problem.
-template <int LAYOUT, int EPI, typename OutT>
+template <int LAYOUT, int EPI, typename OutT, int BM = BT_M>
 __global__ __launch_bounds__(512, 2) void gemm_bf16_8ph_pair(GemmArgs p0, GemmArgs p1) {
-  const int nt0 = (p0.M / BT_M) * (p0.N / BT_N);
+  const int nt0 = (p0.M / BM) * (p0.N / BT_N);
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int which = bid >= nt0 ? 1 : 0;  // one inlined body over the selected argument block (code size)
-  gemm_8ph_body<LAYOUT, EPI, OutT, true, -1, 8, false, true>(which ? p1 : p0, which, bid - which * nt0);
+  gemm_8ph_body<LAYOUT, EPI, OutT, true, -1, 8, false, true, BM>(which ? p1 : p0, which, bid - which * nt0);
+}
+
+// 224-row tiles (see gemm_8ph_body): one tile per block, staggered 8-phase main loop
+template <int LAYOUT, int EPI, typename OutT, int ACT = -1>
+__global__ __launch_bounds__(512, 2) void gemm_bf16_8ph_m224(GemmArgs p) {
+  gemm_8ph_body<LAYOUT, EPI, OutT, true, ACT, 8, false, false, 224>(p, 0, blockIdx.x);
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -1996,6 +2059,7 @@ static hipError_t dispatch_epi(int path, int epi, const GemmArgs& a, int in_dt, 
   case E:                                                           \
     if (path == 0) return launch_bf16<L, E>(a, out_dt, s);          \
     if (path == 1) return launch_f32<L, E>(a, s);                   \
+    if (path == 3) return launch_m224<L, E>(a, out_dt, s);          \
     return launch_generic<L, E>(a, in_dt, out_dt, s);
   switch (epi) {
     DLLM_EPI_CASE(EPI_STORE)
@@ -2037,12 +2101,49 @@ static hipError_t dispatch_opt(int path, const GemmArgs& a, int in_dt, hipStream
 }
 
 
-// grouped weight-gradient pair (gemm_bf16_8ph_pair): TN layout, one tile per block, any wgrad epilogue
-template <int E, typename OutT>
+// grouped weight-gradient pair (gemm_bf16_8ph_pair): one tile per block, any wgrad epilogue.  TN (256-row tiles) or NN
+// with 224-row tiles (the transposed-activation TP layout, models/ffn.py: dW2ᵀ = aᵀ·dy and dW1 = daᵀ·x, M = F/tp)
+template <int L, int E, typename OutT, int BM>
 static hipError_t launch_pair(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s) {
-  const int nb = (a0.M / BT_M) * (a0.N / BT_N) + (a1.M / BT_M) * (a1.N / BT_N);
-  hipLaunchKernelGGL((gemm_bf16_8ph_pair<L_TN, E, OutT>), dim3(nb), dim3(512), 0, s, a0, a1);
+  const int nb = (a0.M / BM) * (a0.N / BT_N) + (a1.M / BM) * (a1.N / BT_N);
+  hipLaunchKernelGGL((gemm_bf16_8ph_pair<L, E, OutT, BM>), dim3(nb), dim3(512), 0, s, a0, a1);
   return hipGetLastError();
+}
+template <int L, int BM>
+static hipError_t dispatch_pair(int epi, const GemmArgs& a0, const GemmArgs& a1, int out_dt, hipStream_t s) {
+  switch (epi) {
+    case EPI_STORE:
+      return out_dt == DT_F32 ? launch_pair<L, EPI_STORE, float, BM>(a0, a1, s)
+                              : launch_pair<L, EPI_STORE, uint16_t, BM>(a0, a1, s);
+    case EPI_SGD: return launch_pair<L, EPI_SGD, float, BM>(a0, a1, s);
+    case EPI_SGDS: return launch_pair<L, EPI_SGDS, float, BM>(a0, a1, s);
+    case EPI_ADAM: return launch_pair<L, EPI_ADAM, float, BM>(a0, a1, s);
+    case EPI_ADAMS: return launch_pair<L, EPI_ADAMS, float, BM>(a0, a1, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// single GEMM on 224-row tiles (path 3): NT / NN, the FFN's forward / dgrad activation epilogues with a compile-time
+// ReLU (others: runtime activation), plain stores and the fused optimizers
+template <int L, int E>
+static hipError_t launch_m224(const GemmArgs& a, int out_dt, hipStream_t s) {
+  if constexpr (L == L_TN || E == EPI_GLU || E == EPI_DGLU) {
+    return hipErrorInvalidValue;
+  } else {
+    const int nb = (a.M / 224) * (a.N / BT_N);
+    constexpr bool opt = E == EPI_SGD || E == EPI_SGDS || E == EPI_ADAM || E == EPI_ADAMS;
+    if constexpr (opt) {
+      hipLaunchKernelGGL((gemm_bf16_8ph_m224<L, E, float>), dim3(nb), dim3(512), 0, s, a);
+    } else {
+      if (out_dt == DT_F32)
+        hipLaunchKernelGGL((gemm_bf16_8ph_m224<L, E, float>), dim3(nb), dim3(512), 0, s, a);
+      else if ((E == EPI_ACT || E == EPI_DACT) && a.act == ACT_RELU)
+        hipLaunchKernelGGL((gemm_bf16_8ph_m224<L, E, uint16_t, ACT_RELU>), dim3(nb), dim3(512), 0, s, a);
+      else
+        hipLaunchKernelGGL((gemm_bf16_8ph_m224<L, E, uint16_t>), dim3(nb), dim3(512), 0, s, a);
+    }
+    return hipGetLastError();
+  }
 }
 
 // per-layout entry points (one translation unit each)
@@ -2051,5 +2152,7 @@ hipError_t dispatch_nn(int path, int epi, const GemmArgs& a, int in_dt, int out_
 hipError_t dispatch_tn(int path, int epi, const GemmArgs& a, int in_dt, int out_dt, hipStream_t s);
 hipError_t dispatch_tn_opt(int path, int epi, const GemmArgs& a, int in_dt, hipStream_t s);
 hipError_t dispatch_tn_pair(int epi, const GemmArgs& a0, const GemmArgs& a1, int out_dt, hipStream_t s);
+hipError_t dispatch_nn_pair(int epi, const GemmArgs& a0, const GemmArgs& a1, int out_dt, hipStream_t s);
+hipError_t dispatch_nn_opt(int epi, const GemmArgs& a, hipStream_t s);
 
 }  // namespace dllm

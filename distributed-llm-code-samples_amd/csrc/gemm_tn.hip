@@ -16,15 +16,7 @@ hipError_t dispatch_tn_opt(int path, int epi, const GemmArgs& a, int in_dt, hipS
 }
 
 hipError_t dispatch_tn_pair(int epi, const GemmArgs& a0, const GemmArgs& a1, int out_dt, hipStream_t s) {
-  switch (epi) {
-    case EPI_STORE:
-      return out_dt == DT_F32 ? launch_pair<EPI_STORE, float>(a0, a1, s) : launch_pair<EPI_STORE, uint16_t>(a0, a1, s);
-    case EPI_SGD: return launch_pair<EPI_SGD, float>(a0, a1, s);
-    case EPI_SGDS: return launch_pair<EPI_SGDS, float>(a0, a1, s);
-    case EPI_ADAM: return launch_pair<EPI_ADAM, float>(a0, a1, s);
-    case EPI_ADAMS: return launch_pair<EPI_ADAMS, float>(a0, a1, s);
-    default: return hipErrorInvalidValue;
-  }
+  return dispatch_pair<L_TN, BT_M>(epi, a0, a1, out_dt, s);
 }
 
 }  // namespace dllm

@@ -177,6 +177,54 @@ def layer_bwd(dy: torch.Tensor, x: torch.Tensor, w1: torch.Tensor, w2: torch.Ten
     return dx
 
 
+# ------------------------------------------------------------------------------------------------------------------
+# Transposed-activation layer (tensor-parallel shards whose F/tp is a multiple of 224 but not of 256, e.g. the MP
+# config's F = 14336 over 8 GPUs: 1792 rows).  The activations are kept as aᵀ / hᵀ / daᵀ [F, T] and W2 as W2ᵀ [F, D],
+# so in every GEMM whose output has an F dimension that dimension is M, which the 224-row tiles cover exactly
+# (F/tp = 8 x 224): h, da -> 8 x 32 = 256 tiles, dW2ᵀ | dW1 -> 128 + 128 tiles in one grouped launch, i.e. the
+# whole chip with no split-K and no idle CU.  The math is the reference layer's (train_ffns.py:54-70, K1-K8) with
+# every [T, F] operand transposed; only NT / NN / TN layouts occur:
+#   hᵀ  = W1·xᵀ           NT  [F, T]   + act epilogue (ReLU bitmask)
+#   y   = (aᵀ)ᵀ·W2ᵀ        TN  [T, D]
+#   daᵀ = W2ᵀ·dyᵀ ⊙ act'   NT  [F, T]   + act' epilogue (bitmask)
+#   dx  = (daᵀ)ᵀ·W1        TN  [T, D]
+#   dW2ᵀ = aᵀ·dy | dW1 = daᵀ·x   NN [F, D] (+ fused optimizer), one grouped launch
+# ------------------------------------------------------------------------------------------------------------------
+def layer_fwd_t(x: torch.Tensor, w1: torch.Tensor, w2t: torch.Tensor, act: str, aT: torch.Tensor,
+                hT: torch.Tensor | None, y_out: torch.Tensor, before_fwd2=None,
+                mask: torch.Tensor | None = None) -> torch.Tensor:
+    """Transposed-activation forward: ``aT = act(W1·xᵀ)`` [F, T], ``y = aTᵀ·W2ᵀ`` [T, D] (``w2t`` = W2ᵀ [F, D])."""
+    gemm(w1, x, "nt", out=aT, epi="act", act=act, aux_out=hT, mask=mask)
+    if before_fwd2 is not None:
+        before_fwd2()
+    gemm(aT, w2t, "tn", out=y_out)
+    return y_out
+
+
+def layer_bwd_t(dy: torch.Tensor, x: torch.Tensor, w1: torch.Tensor, w2t: torch.Tensor, act: str, aT: torch.Tensor,
+                hT: torch.Tensor | None, gw1, gw2, daT: torch.Tensor, dx_out: torch.Tensor | None, hooks=None,
+                mask: torch.Tensor | None = None) -> torch.Tensor | None:
+    """Transposed-activation backward (order ``da, dx, dW2 | dW1``: dx reads W1 before its fused update, a TP
+    all-reduce of dx overlaps the grouped weight-gradient launch).  ``gw2`` targets W2ᵀ [F, D]."""
+    gemm(w2t, dy, "nt", out=daT, epi="dact", act=act, aux=hT if hT is not None else aT, mask=mask)
+    dx = None
+    if dx_out is not None:
+        dx = gemm(daT, w1, "tn", out=dx_out)                           # dx = da·W1        [T, D]
+        if hooks is not None:
+            hooks.after_dx(dx)
+    kw1 = gw1 if isinstance(gw1, dict) else {"out": gw1}
+    kw2 = gw2 if isinstance(gw2, dict) else {"out": gw2}
+    gemm_pair(aT, dy, kw2, daT, x, kw1, layout="nn")                   # dW2ᵀ = aᵀ·dy | dW1 = daᵀ·x   [F, D]
+    if hooks is not None:
+        if dx_out is None:   # layer 0's completion order (flat layout): W1 first
+            hooks.after_w1()
+            hooks.after_w2()
+        else:
+            hooks.after_w2()
+            hooks.after_w1()
+    return dx
+
+
 def recompute_fwd1(x: torch.Tensor, w1: torch.Tensor, act: str, gated: bool, a_out: torch.Tensor,
                    h_out: torch.Tensor | None, mask: torch.Tensor | None = None) -> None:
     """Reference-style activation recompute (train_ffns.py:63,66) for ``recompute='full'``."""

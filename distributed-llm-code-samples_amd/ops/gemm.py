@@ -37,7 +37,7 @@ from .master import join_master, set_master_
 
 LAYOUTS = {"nt": 0, "nn": 1, "tn": 2}
 EPIS = {"store": 0, "act": 1, "dact": 2, "glu": 3, "dglu": 4, "sgd": 5, "adam": 6, "sgd_split": 7, "adam_split": 8}
-FORCE = {None: -1, "mfma_bf16": 0, "mfma_f32": 1, "generic": 2, "bf16x6": -1}
+FORCE = {None: -1, "mfma_bf16": 0, "mfma_f32": 1, "generic": 2, "bf16x6": -1, "mfma_bf16_m224": 3}
 
 
 def gemm_shape(a: torch.Tensor, b: torch.Tensor, layout: str) -> tuple[int, int, int]:
@@ -268,8 +268,10 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
         raise ValueError(f"epilogue {epi} needs aux (pre-activation)")
     if epi == "glu" and N % 32:
         raise ValueError("gated GEMM needs N % 32 == 0 (16-row interleave)")
+    # fused optimizers: the weight-gradient layouts -- TN, or NN on 224-row tiles (transposed-activation TP layout)
+    opt_layout_ok = layout == "tn" or (layout == "nn" and M % 256 != 0 and M % 224 == 0 and a.device.type == "cuda")
     if epi in ("sgd", "adam"):
-        if layout != "tn" or out.dtype != torch.float32:
+        if not (opt_layout_ok or (layout == "nn" and a.device.type != "cuda")) or out.dtype != torch.float32:
             raise ValueError("fused-optimizer epilogues need the TN (weight-gradient) layout and an fp32 master")
         if epi == "adam" and (opt_m is None or opt_v is None or step < 1):
             raise ValueError("adam epilogue needs opt_m, opt_v and step >= 1")
@@ -279,7 +281,8 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
     if epi in ("sgd_split", "adam_split"):
         if epi == "adam_split" and (opt_m is None or opt_v is None or step < 1):
             raise ValueError("adam_split epilogue needs opt_m, opt_v and step >= 1")
-        if layout != "tn" or out.dtype != torch.int16 or aux_out is None or aux_out.dtype != torch.bfloat16 \
+        if not (opt_layout_ok or (layout == "nn" and a.device.type != "cuda")) or out.dtype != torch.int16 \
+                or aux_out is None or aux_out.dtype != torch.bfloat16 \
                 or aux_out.shape != out.shape or a.dtype != torch.bfloat16:
             raise ValueError(f"{epi} needs the TN layout, bf16 operands, an int16 residual plane as out and its "
                              "bf16 working copy as aux_out")
@@ -346,33 +349,46 @@ def set_pair_wgrads(enabled: bool) -> bool:
     return old
 
 
-def pair_supported(shapes, dtype: torch.dtype = torch.bfloat16) -> bool:
-    """Whether two TN GEMMs ``shapes = ((M0, N0, K), (M1, N1, K))`` run as one grouped launch: bf16, 256-tiled, the
-    8-phase K step, both tile grids together <= the CUs, and each alone small enough that it would run split-K (a
-    part-empty chip plus a reduction pass) -- e.g. the MP (TP8) shard's dW2 [4096, 1792] and dW1 [1792, 4096]."""
+def tile_rows(M: int) -> int:
+    """Output-tile rows of the bf16 MFMA kernels for an M dimension: 256, or 224 for M = 224k not 256-tiled (the
+    MP / TP8 shard's F/8 = 1792 rows; K-contiguous A layouts only)."""
+    return 256 if M % 256 == 0 else 224
+
+
+def pair_supported(shapes, dtype: torch.dtype = torch.bfloat16, layout: str = "tn") -> bool:
+    """Whether two weight-gradient GEMMs ``shapes = ((M0, N0, K), (M1, N1, K))`` run as one grouped launch: bf16, the
+    8-phase K step, both tile grids together <= the CUs, and each alone too small to fill the chip.  ``"tn"``: 256-row
+    tiles, each GEMM would otherwise run split-K (a part-empty chip plus a reduction pass) -- e.g. the MP (TP8) shard's
+    dW2 [4096, 1792] and dW1 [1792, 4096].  ``"nn"``: 224-row tiles (the transposed-activation TP layout's dW2ᵀ and dW1,
+    both [1792, 4096]: 128 + 128 tiles, exactly the 256 CUs)."""
     (M0, N0, K0), (M1, N1, K1) = shapes
     if not _PAIR["enabled"] or dtype != torch.bfloat16 or K0 != K1 or K0 % 128:
         return False
-    if any(m % 256 or n % 256 for m, n in ((M0, N0), (M1, N1))):
-        return False
     if _VARIANT["name"] not in ("auto", "8phase_stagger"):
+        return False
+    if layout == "nn":
+        if any(m % 224 or m % 256 == 0 or n % 256 for m, n in ((M0, N0), (M1, N1))):
+            return False
+        return (M0 // 224) * (N0 // 256) + (M1 // 224) * (N1 // 256) <= NUM_CUS
+    if any(m % 256 or n % 256 for m, n in ((M0, N0), (M1, N1))):
         return False
     tiles = (M0 // 256) * (N0 // 256) + (M1 // 256) * (N1 // 256)
     return tiles <= NUM_CUS and (choose_ksplit(M0, N0, K0) > 1 or choose_ksplit(M1, N1, K1) > 1)
 
 
-def gemm_pair(a0: torch.Tensor, b0: torch.Tensor, kw0: dict, a1: torch.Tensor, b1: torch.Tensor, kw1: dict) -> None:
-    """Two weight-gradient (TN) GEMMs ``gemm(a0, b0, "tn", **kw0)`` and ``gemm(a1, b1, "tn", **kw1)`` -- same epilogue
-    and K -- as ONE grouped launch with one 256x256 tile per block (``csrc/gemm_kernels.h`` ``gemm_bf16_8ph_pair``).
-    Each result is bitwise the unsplit single GEMM's.  Falls back to two ``gemm`` calls where the grouped kernel does
-    not apply (CPU tensors, shapes, alignment)."""
-    M0, N0, K0 = gemm_shape(a0, b0, "tn")
-    M1, N1, K1 = gemm_shape(a1, b1, "tn")
+def gemm_pair(a0: torch.Tensor, b0: torch.Tensor, kw0: dict, a1: torch.Tensor, b1: torch.Tensor, kw1: dict,
+              layout: str = "tn") -> None:
+    """Two weight-gradient GEMMs ``gemm(a0, b0, layout, **kw0)`` and ``gemm(a1, b1, layout, **kw1)`` -- same epilogue
+    and K -- as ONE grouped launch with one tile per block (``csrc/gemm_kernels.h`` ``gemm_bf16_8ph_pair``; ``"tn"``
+    on 256x256 tiles, ``"nn"`` on 224x256 tiles).  Each result is bitwise the single unsplit GEMM's.  Falls back to two
+    ``gemm`` calls where the grouped kernel does not apply (CPU tensors, shapes, alignment)."""
+    M0, N0, K0 = gemm_shape(a0, b0, layout)
+    M1, N1, K1 = gemm_shape(a1, b1, layout)
     epi = kw0.get("epi", "store")
     if a0.device.type != "cuda" or kw1.get("epi", "store") != epi or not pair_supported(((M0, N0, K0), (M1, N1, K1)),
-                                                                                         a0.dtype):
-        gemm(a0, b0, "tn", **kw0)
-        gemm(a1, b1, "tn", **kw1)
+                                                                                         a0.dtype, layout):
+        gemm(a0, b0, layout, **kw0)
+        gemm(a1, b1, layout, **kw1)
         return
     for kw in (kw0, kw1):
         bad = set(kw) - {"out", "epi", "lr", "aux_out", "betas", "eps", "wd", "step", "opt_m", "opt_v", "alpha"}
@@ -408,7 +424,7 @@ def gemm_pair(a0: torch.Tensor, b0: torch.Tensor, kw0: dict, a1: torch.Tensor, b
     obs = _observe.active()
     if obs is not None:
         obs.gemm_begin()
-    rc = L.dllm_gemm_pair(out_dt, EPIS[epi], arr(c_void_p, [a0.data_ptr(), a1.data_ptr()]),
+    rc = L.dllm_gemm_pair(LAYOUTS[layout], out_dt, EPIS[epi], arr(c_void_p, [a0.data_ptr(), a1.data_ptr()]),
                           arr(c_long, [a0.stride(0), a1.stride(0)]), arr(c_void_p, [b0.data_ptr(), b1.data_ptr()]),
                           arr(c_long, [b0.stride(0), b1.stride(0)]), arr(c_void_p, [o.data_ptr() for o in outs]),
                           arr(c_long, [o.stride(0) for o in outs]), arr(c_void_p, [ptr(t) for t in aux]),
@@ -421,21 +437,23 @@ def gemm_pair(a0: torch.Tensor, b0: torch.Tensor, kw0: dict, a1: torch.Tensor, b
     if obs is not None:
         obs.gemm_end()
     if rc == -1:   # not expressible as one grouped launch (alignment, CU count): two GEMMs
-        gemm(a0, b0, "tn", **kw0)
-        gemm(a1, b1, "tn", **kw1)
+        gemm(a0, b0, layout, **kw0)
+        gemm(a1, b1, layout, **kw1)
         return
     _native.check(rc, f"dllm_gemm_pair({epi},{(M0, N0)},{(M1, N1)},K={K0})")
 
 
 def relu_mask_bytes(M: int, N: int) -> int:
-    """Size of the ReLU bitmask of an ``[M, N]`` activation (8 KiB per 256x256 tile)."""
-    return (M // 256) * (N // 256) * 8192
+    """Size of the ReLU bitmask of an ``[M, N]`` activation (8 KiB per 256x256 or 224x256 tile)."""
+    return (M // tile_rows(M)) * (N // 256) * 8192
 
 
 def relu_mask_supported(M: int, N: int, K: int, dtype: torch.dtype = torch.bfloat16) -> bool:
     """Whether the forward (``x·W1ᵀ``, K = D) / dgrad (``dy·W2``, K = D) pair of an ``[M, N]`` ReLU activation runs
     on the 8-phase kernels that share the bitmask's tile-native layout."""
     kstep = 64 if _VARIANT["name"] == "pp" else 128
+    if dtype == torch.bfloat16 and M % 256 and M % 224 == 0 and N % 256 == 0 and K % 128 == 0:
+        return _VARIANT["name"] in ("auto", "8phase_stagger")   # 224-row tiles (transposed-activation TP layout)
     return (dtype == torch.bfloat16 and M % 256 == 0 and N % 256 == 0 and K % kstep == 0
             and choose_ksplit(M, N, K) == 1 and _VARIANT["name"] != "2stage")
 
@@ -491,4 +509,4 @@ def gemm_path(a_dtype: torch.dtype, out_dtype: torch.dtype, M: int, N: int, K: i
     """Which native kernel family a call would use: 'mfma_bf16', 'mfma_f32' or 'generic'."""
     p = _native.lib().dllm_gemm_path(_native.dtype_code(a_dtype), _native.dtype_code(out_dtype), M, N, K,
                                      lda, ldb, ldc)
-    return {0: "mfma_bf16", 1: "mfma_f32", 2: "generic"}[p]
+    return {0: "mfma_bf16", 1: "mfma_f32", 2: "generic", 3: "mfma_bf16_m224"}[p]

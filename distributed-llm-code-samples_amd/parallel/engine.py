@@ -42,7 +42,8 @@ from dataclasses import dataclass
 
 import torch
 
-from ..models.ffn import (deinterleave_w13, interleave_w13, layer_bwd, layer_fwd, needs_preact,
+from ..models.ffn import (deinterleave_w13, interleave_w13, layer_bwd, layer_bwd_t, layer_fwd, layer_fwd_t,
+                          needs_preact,
                           recompute_fwd1)
 from ..ops.elementwise import adam_split_step_, adam_step_, cast_, sgd_split_step_, sgd_step_
 from ..ops.master import join_flat, part_flat, split_master
@@ -146,6 +147,11 @@ class FFNTrainer:
         if self.sp and T % t:
             raise ValueError("sequence parallelism needs tokens % tp == 0")
         self.T = T
+        # transposed-activation layout (models/ffn.layer_fwd_t): F/tp = 224k not 256-tiled (MP at tp 8: 1792), so the
+        # F-sized GEMM dimensions run on 224-row tiles; activations [F, T], W2 stored as W2ᵀ [F, D]
+        self.tmode = (cfg.tp_transposed and self.device.type == "cuda" and not self.gated and not self.fsdp
+                      and not self.zero and not self.sp and cfg.recompute == "none" and self.cd == torch.bfloat16
+                      and self.F_loc % 256 != 0 and self.F_loc % 224 == 0 and T % 256 == 0 and D % 256 == 0)
         self.step_count = 0
         dev = self.device
         if dev.type == "cuda":
@@ -173,7 +179,7 @@ class FFNTrainer:
             mesh.groups["tp_car"] = self.tp_car
 
         # ---- flat owned parameter layout (completion order) ------------------------------------
-        full = {"w2": (D, self.F_loc), "w1": (self.R1, D)}
+        full = {"w2": (self.F_loc, D) if self.tmode else (D, self.F_loc), "w1": (self.R1, D)}
         self.entries: list[Entry] = []
         off = 0
         # ZeRO shards every bucket evenly over dp ranks: keep every entry a multiple of dp*ALIGN
@@ -267,18 +273,21 @@ class FFNTrainer:
                             torch.empty((Tl, D), dtype=self.cd, device=dev) for _ in range(L)]
         keep = cfg.recompute == "none"
         nA = L if keep else 1
-        self.acts_a = [torch.empty((T, self.F_loc), dtype=self.cd, device=dev) for _ in range(nA)]
+        ash = (self.F_loc, T) if self.tmode else (T, self.F_loc)      # transposed mode: [F, T]
+        self.acts_a = [torch.empty(ash, dtype=self.cd, device=dev) for _ in range(nA)]
         self.need_h = needs_preact(self.act, self.gated)
-        self.acts_h = ([torch.empty((T, self.R1), dtype=self.cd, device=dev) for _ in range(nA)]
+        hsh = (self.R1, T) if self.tmode else (T, self.R1)
+        self.acts_h = ([torch.empty(hsh, dtype=self.cd, device=dev) for _ in range(nA)]
                        if self.need_h else None)
-        self.da = torch.empty((T, self.R1), dtype=self.cd, device=dev)
+        self.da = torch.empty(hsh, dtype=self.cd, device=dev)
         # ReLU: 1-bit activation-gradient masks (written by the forward's first GEMM, read by the dgrad)
         self.masks = None
         if cfg.relu_mask and self.act == "relu" and not self.gated and dev.type == "cuda":
             from ..ops.gemm import relu_mask_bytes, relu_mask_supported
 
-            if relu_mask_supported(T, self.F_loc, D, self.cd):
-                self.masks = [torch.empty(relu_mask_bytes(T, self.F_loc), dtype=torch.uint8, device=dev)
+            mM, mN = (self.F_loc, T) if self.tmode else (T, self.F_loc)
+            if relu_mask_supported(mM, mN, D, self.cd):
+                self.masks = [torch.empty(relu_mask_bytes(mM, mN), dtype=torch.uint8, device=dev)
                               for _ in range(nA)]
         # TP forward row chunks (see TrainConfig.tp_chunks): whole 256-row tiles per chunk; the ReLU bitmask is
         # written per chunk (tile-native layout, tile rows contiguous), so chunk GEMMs must stay on its kernels
@@ -289,7 +298,7 @@ class FFNTrainer:
         c = max(1, cfg.tp_chunks)
         if dev.type == "cuda":
             c = gpu_chunk_count(T, D, self.F_loc, self.R1, c)
-        if self.tp_comm and not self.sp and c > 1 and T % (256 * c) == 0 and L > 1:
+        if self.tp_comm and not self.sp and not self.tmode and c > 1 and T % (256 * c) == 0 and L > 1:
             if self.masks is None:
                 self.tp_chunks = c
             else:
@@ -325,7 +334,7 @@ class FFNTrainer:
         # run split-K plus a reduction pass): both in one launch of whole tiles, after dx (models/ffn.layer_bwd).  It
         # replaces the weight-gradient stream there: two part-empty grids have no tail worth filling
         self.pair_wgrads = False
-        if dev.type == "cuda":
+        if dev.type == "cuda" and not self.tmode:
             from ..ops.gemm import pair_supported
 
             self.pair_wgrads = pair_supported(((D, self.F_loc, T), (self.R1, D, T)), self.cd)
@@ -333,7 +342,8 @@ class FFNTrainer:
         wg_tiles = -(-self.R1 // 256) * -(-D // 256)
         ncu = torch.cuda.get_device_properties(dev).multi_processor_count if dev.type == "cuda" else 256
         if (cfg.wgrad_stream and self.fused_opt and dev.type == "cuda" and not self.tp_comm and not self.sp
-                and cfg.recompute == "none" and wg_tiles <= cfg.wgrad_stream_max_tpc * ncu and not self.pair_wgrads):
+                and cfg.recompute == "none" and wg_tiles <= cfg.wgrad_stream_max_tpc * ncu and not self.pair_wgrads
+                and not self.tmode):
             self.wg_stream = self._side_stream("wgrad")
             self.da_ring = [self.da, torch.empty_like(self.da)]
             self.da_free = [None, None]
@@ -370,6 +380,12 @@ class FFNTrainer:
     # ------------------------------------------------------------------------------------------------
     def _view(self, flat: torch.Tensor, e: Entry) -> torch.Tensor:
         return flat[e.offset:e.offset + e.numel].view(e.shape)
+
+    def logical_view(self, flat: torch.Tensor, e: Entry) -> torch.Tensor:
+        """The stored 2-D tensor of ``e`` in the logical [out, in] orientation (a transposed view of W2ᵀ in the
+        transposed-activation layout; checkpoints read and write through it)."""
+        v = self._view(flat, e)
+        return v.t() if (self.tmode and e.name == "w2") else v
 
     @property
     def master(self) -> torch.Tensor:
@@ -516,6 +532,8 @@ class FFNTrainer:
         if self.gated:
             w1 = interleave_w13(w1, p["w3"][r * Fl:(r + 1) * Fl])
         w2 = p["w2"][:, r * Fl:(r + 1) * Fl]
+        if self.tmode:
+            w2 = w2.t().contiguous()   # stored as W2ᵀ [F_loc, D]
         return {"w1": w1, "w2": w2}
 
     def flat_buffers(self) -> dict:
@@ -633,6 +651,8 @@ class FFNTrainer:
             for name in ("w1", "w2"):
                 e = self.entry[(l, name)]
                 mv = self.master_slice(e.offset, e.offset + e.numel).view(e.shape) if per_entry else self._view(src, e)
+                if self.tmode and name == "w2":
+                    mv = mv.t()   # logical [D, F_loc] from the stored W2ᵀ
                 if self.fsdp:
                     full = torch.empty(self.entry[(l, name)].full_shape, dtype=torch.float32, device=self.device)
                     comm.all_gather_into(full, mv.contiguous(), self.mesh.group("dp_ag"), async_op=False)
@@ -968,8 +988,11 @@ class FFNTrainer:
                 if self.tp_chunks > 1:
                     self._tp_fwd_chunked(l, w1, w2, a, h, before2)
                     continue
-                layer_fwd(self.xs[l], w1, w2, act, gated, a, h, self.xs[l + 1], before_fwd2=before2,
-                          mask=self._mask(l))
+                if self.tmode:
+                    layer_fwd_t(self.xs[l], w1, w2, act, a, h, self.xs[l + 1], before_fwd2=before2, mask=self._mask(l))
+                else:
+                    layer_fwd(self.xs[l], w1, w2, act, gated, a, h, self.xs[l + 1], before_fwd2=before2,
+                              mask=self._mask(l))
                 if self.tp_comm:
                     if self.tp_car is not None:
                         w = self.tp_car.all_reduce_async(self.xs[l + 1])
@@ -1044,6 +1067,11 @@ class FFNTrainer:
                     g = self.dxs[l % 2]
             elif self.wg_stream is not None:
                 g = self._layer_bwd_concurrent(l, g, w1, w2, a, h, gw1, gw2, need_dx)
+            elif self.tmode:
+                dx = layer_bwd_t(g, self.xs[l], w1, w2, act, a, h, gw1, gw2, self.da,
+                                 self.dxb[l % 2] if need_dx else None, hooks, mask=self._mask(l))
+                if dx is not None:
+                    g = dx
             else:
                 if not keep:
                     recompute_fwd1(self.xs[l], w1, act, gated, a, h, mask=self._mask(l))

@@ -153,7 +153,7 @@ def save_checkpoint(eng, path: str, step: int, fmt: str = "consolidated", meta: 
                     t = flat[p["src"]:p["src"] + (p["e1"] - p["e0"])]
                 else:
                     e = eng.entry[(p["layer"], p["name"])]
-                    own = eng._view(flat, e)  # the stored 2-D tensor (FSDP: its row shard)
+                    own = eng.logical_view(flat, e)  # the stored 2-D tensor, [out, in] (FSDP: its row shard)
                     lo = p["r0"] - (p["r0"] if eng.fsdp else 0)
                     t = own[lo:lo + (p["r1"] - p["r0"])]
                 tensors[key] = t.detach().to(torch.float32).contiguous().cpu()
@@ -216,7 +216,7 @@ def _fill(eng, target: torch.Tensor, e, sources, reader: _Reader) -> int:
                 continue
             blk = read(a, b, c, d).to(device=target.device, dtype=target.dtype)  # [b-a, d-c]
             if dest[0] == "rows":  # the stored 2-D view (FSDP: its row shard) starts at global row R0
-                eng._view(target, e)[(a - R0):(b - R0), (c - C0):(d - C0)].copy_(blk)
+                eng.logical_view(target, e)[(a - R0):(b - R0), (c - C0):(d - C0)].copy_(blk)
             else:
                 _, start, lr0, lc0, cols = dest
                 # box rows are local rows lr0.. of the flat segment; flat index of (row, col) relative to

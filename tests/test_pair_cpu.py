@@ -61,3 +61,28 @@ def test_pair_schedule_fused_sgd_reads_old_w1_for_dx():
                    {"out": w2f, "epi": "sgd", "lr": 0.1}, torch.empty_like(h), torch.empty_like(x), pair_wgrads=True)
     assert torch.allclose(dx, ref, rtol=0, atol=1e-6)
     assert not torch.equal(w1f, w1)
+
+
+def test_transposed_activation_layer_matches_reference_layer():
+    """layer_fwd_t / layer_bwd_t (activations [F, T], W2 stored as W2ᵀ) compute the reference layer's y, dx, dW1, dW2
+    (train_ffns.py:54-70) -- checked in fp64 on CPU against layer_fwd / layer_bwd."""
+    from dllm.models.ffn import layer_bwd_t, layer_fwd, layer_fwd_t
+
+    x, w1, w2, dy, a, h = _layer(3)
+    T, F = a.shape
+    D = x.shape[1]
+    y = torch.empty(T, D, dtype=torch.float64)
+    layer_fwd(x, w1, w2, "relu", False, torch.empty(T, F, dtype=torch.float64), None, y)
+    yt = torch.empty_like(y)
+    aT = torch.empty(F, T, dtype=torch.float64)
+    layer_fwd_t(x, w1, w2.t().contiguous(), "relu", aT, None, yt)
+    assert torch.allclose(yt, y, rtol=1e-12, atol=1e-12) and torch.allclose(aT.t(), a)
+    gw1, gw2 = torch.empty_like(w1), torch.empty_like(w2)
+    dx = layer_bwd(dy, x, w1, w2, "relu", False, a, None, gw1, gw2, torch.empty_like(h), torch.empty_like(x))
+    gw1t, gw2t = torch.empty_like(w1), torch.empty(F, D, dtype=torch.float64)
+    rec = _Rec()
+    dxt = layer_bwd_t(dy, x, w1, w2.t().contiguous(), "relu", aT, None, gw1t, gw2t, torch.empty(F, T, dtype=torch.float64),
+                      torch.empty_like(x), rec)
+    assert torch.allclose(dxt, dx, rtol=1e-12, atol=1e-12)
+    assert torch.allclose(gw1t, gw1, rtol=1e-12, atol=1e-12) and torch.allclose(gw2t.t(), gw2, rtol=1e-12, atol=1e-12)
+    assert rec.ev == ["dx", "w2", "w1"]
