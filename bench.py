@@ -376,6 +376,8 @@ def _run_on_mesh(a, method, cfg, mesh, n, world, dev, steps, warmup, force_comm,
            "global_batch": a.batch_size * dp, "parallelism": parallelism(method, n, dp, tp, world, force_comm),
            "model": model_name(model), "steps": steps, "warmup": warmup, "state_gib": state_gib(eng),
            "wgrad_stream": eng.wg_stream is not None,
+           # small-grid weight gradients in one grouped launch / F-major activations on 224-row tiles (MP at tp 8)
+           "pair_wgrads": bool(eng.pair_wgrads), "tp_transposed": bool(eng.tmode),
            # the ranks each role communicator actually spans (RCCL / gloo group sizes; {} = no collective)
            "comm_sizes": {role: g.size() for role, g in mesh.groups.items() if g is not None}}
     if phases:
@@ -434,7 +436,7 @@ def _run_on_mesh(a, method, cfg, mesh, n, world, dev, steps, warmup, force_comm,
 
 
 SIDE_KEYS = ("value", "ms_per_step", "tflops_per_gpu", "peak_hbm_gib", "parallelism", "model", "global_batch",
-             "steps", "finite", "state_gib", "comm", "queues", "comm_sizes")
+             "steps", "finite", "state_gib", "comm", "queues", "comm_sizes", "pair_wgrads", "tp_transposed")
 
 
 def main(argv=None) -> int:
