@@ -4,7 +4,7 @@
 # the driver's N=1 command (queues, exposed_ms_diff), kernel traces (TP8 shard; headline with a live communicator).
 source scripts/gpu_steps.sh
 { echo "GPU_MAX_HW_QUEUES=${GPU_MAX_HW_QUEUES-<unset>}"; env | grep -E '^(HIP|HSA|GPU|NCCL|RCCL|OMP)_' | sort; } > gpurun_out/env.txt 2>&1
-step pytest_new 900 python -u -m pytest -x -v --timeout 180 --timeout-method thread tests/test_m224_gpu.py tests/test_gemm_pair_gpu.py tests/test_streams_gpu.py "tests/test_engine_gpu.py::test_overlapped_data_mismatched_seed_bitwise" "tests/test_gemm_gpu.py::test_rng_matches_cpu_philox"
+step pytest_new 900 python -u -m pytest -x -v --timeout 180 --timeout-method thread tests/test_m224_gpu.py tests/test_gemm_pair_gpu.py tests/test_streams_gpu.py "tests/test_engine_gpu.py::test_overlapped_data_mismatched_seed_bitwise" "tests/test_split_master_gpu.py::test_fused_sgd_split_faulting_shape_of_parked_seam_patch" "tests/test_gemm_gpu.py::test_rng_matches_cpu_philox"
 step rng 120 python -u scripts/bench_rng.py
 TP="python -u bench.py --methods none --method tp --ffn_dim 1792 --layers 1 --steps 20 --warmup 5"
 for r in 1 2; do

@@ -45,6 +45,19 @@ def test_fused_sgd_split_equals_fp32_master(variant, tpb):
         set_tiles_per_block(old_t)
 
 
+def test_fused_sgd_split_faulting_shape_of_parked_seam_patch():
+    """The shape whose deferred-SGD experiment faulted in round 3 (4096 x 8192 x 4352, tpb 8; parked patch
+    experiments/seam_and_defer_sgd.patch) on the SHIPPED persistent fused-SGD path: clean and bitwise equal to the fp32
+    master form."""
+    old_v, old_t = set_bf16_variant("8phase_stagger"), set_tiles_per_block(8)
+    try:
+        a, b, w = _pair(4096, 8192, 4352, 12)
+        _check_same_update(a, b, w)
+    finally:
+        set_bf16_variant(old_v)
+        set_tiles_per_block(old_t)
+
+
 def test_fused_sgd_split_splitk_and_generic():
     set_splitk(True)
     a, b, w = _pair(512, 512, 2048, 6)         # 4 tiles -> split-K reduction applies the update
