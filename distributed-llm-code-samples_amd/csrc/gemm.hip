@@ -17,6 +17,19 @@ static int pp_skew() {
   return skew;
 }
 
+// 224-row tiles instead of 256-row ones for an M x N output: M = 224k, and the 224-row grid fills the device's CUs
+// strictly better (fraction of the last wave of tiles in use); mirrored by ops/gemm.py use_m224
+static bool use_m224(int M, int N) {
+  if (M % 224 != 0 || N % BT_N != 0) return false;
+  if (M % BT_M != 0) return true;
+  const long ncu = num_cu() > 0 ? num_cu() : 256;
+  auto fill = [&](int bm) {
+    const long t = (long)(M / bm) * (N / BT_N);
+    return (double)t / (double)(((t + ncu - 1) / ncu) * ncu);
+  };
+  return fill(224) > fill(BT_M);
+}
+
 extern "C" {
 
 // Returns 0 on success, a hipError_t otherwise, or -1 for a bad argument.
@@ -64,9 +77,10 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
                            (!split_epi || (ldc % 8 == 0 && ldaux % 8 == 0));
   if (in_dtype == DT_BF16 && M % BT_M == 0 && N % BT_N == 0 && K % BT_K == 0 && aligned_lds) path = 0;
   if (in_dtype == DT_F32 && out_dtype == DT_F32 && M % FT == 0 && N % FT == 0 && K % FK == 0 && aligned_lds) path = 1;
-  // 224-row tiles: M = 224 * k but not 256-tiled (the MP / TP8 shard's F/8 rows), K-contiguous A, 8-phase K step
-  if (in_dtype == DT_BF16 && M % BT_M != 0 && M % 224 == 0 && N % BT_N == 0 && K % (2 * BT_K) == 0 && aligned_lds &&
-      layout != L_TN && epi != EPI_GLU && epi != EPI_DGLU && ksplit <= 1 && variant != 5)
+  // 224-row tiles where they fill the CUs better than 256-row tiles (the MP / TP8 shard's F/8 = 1792 rows: 8 x 224
+  // = 256 tiles per 32 column tiles vs 7 x 256 = 224), K-contiguous A, 8-phase K step
+  if (in_dtype == DT_BF16 && use_m224(M, N) && K % (2 * BT_K) == 0 && aligned_lds && layout != L_TN &&
+      epi != EPI_GLU && epi != EPI_DGLU && ksplit <= 1 && variant != 5)
     path = 3;
   if (force_path >= 0) {
     if (force_path == 0 && path != 0) return -1;
@@ -169,8 +183,8 @@ int dllm_gemm_pair(int layout, int out_dtype, int epi, const void* const* A, con
 // which kernel family dllm_gemm would pick (for tests / profiling labels; 224-row tiles need a K-contiguous A too)
 int dllm_gemm_path(int in_dtype, int out_dtype, int M, int N, int K, long lda, long ldb, long ldc) {
   const bool al = (lda % 8 == 0) && (ldb % 8 == 0) && (ldc % 4 == 0);  // (bases: checked per call)
+  if (in_dtype == DT_BF16 && use_m224(M, N) && K % (2 * BT_K) == 0 && al) return 3;
   if (in_dtype == DT_BF16 && M % BT_M == 0 && N % BT_N == 0 && K % BT_K == 0 && al) return 0;
-  if (in_dtype == DT_BF16 && M % 224 == 0 && N % BT_N == 0 && K % (2 * BT_K) == 0 && al) return 3;
   if (in_dtype == DT_F32 && out_dtype == DT_F32 && M % FT == 0 && N % FT == 0 && K % FK == 0 && al) return 1;
   return 2;
 }

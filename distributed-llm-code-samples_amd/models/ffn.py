@@ -178,8 +178,8 @@ def layer_bwd(dy: torch.Tensor, x: torch.Tensor, w1: torch.Tensor, w2: torch.Ten
 
 
 # ------------------------------------------------------------------------------------------------------------------
-# Transposed-activation layer (tensor-parallel shards whose F/tp is a multiple of 224 but not of 256, e.g. the MP
-# config's F = 14336 over 8 GPUs: 1792 rows).  The activations are kept as aᵀ / hᵀ / daᵀ [F, T] and W2 as W2ᵀ [F, D],
+# Transposed-activation layer (tensor-parallel shards whose F/tp is a multiple of 224 that 224-row tiles cover better
+# than 256-row ones, e.g. the MP config's F = 14336 over 8 GPUs: 1792 = 8 x 224 = 7 x 256 rows).  The activations are kept as aᵀ / hᵀ / daᵀ [F, T] and W2 as W2ᵀ [F, D],
 # so in every GEMM whose output has an F dimension that dimension is M, which the 224-row tiles cover exactly
 # (F/tp = 8 x 224): h, da -> 8 x 32 = 256 tiles, dW2ᵀ | dW1 -> 128 + 128 tiles in one grouped launch, i.e. the
 # whole chip with no split-K and no idle CU.  The math is the reference layer's (train_ffns.py:54-70, K1-K8) with

@@ -269,7 +269,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
     if epi == "glu" and N % 32:
         raise ValueError("gated GEMM needs N % 32 == 0 (16-row interleave)")
     # fused optimizers: the weight-gradient layouts -- TN, or NN on 224-row tiles (transposed-activation TP layout)
-    opt_layout_ok = layout == "tn" or (layout == "nn" and M % 256 != 0 and M % 224 == 0 and a.device.type == "cuda")
+    opt_layout_ok = layout == "tn" or (layout == "nn" and use_m224(M, N) and a.device.type == "cuda")
     if epi in ("sgd", "adam"):
         if not (opt_layout_ok or (layout == "nn" and a.device.type != "cuda")) or out.dtype != torch.float32:
             raise ValueError("fused-optimizer epilogues need the TN (weight-gradient) layout and an fp32 master")
@@ -349,10 +349,25 @@ def set_pair_wgrads(enabled: bool) -> bool:
     return old
 
 
-def tile_rows(M: int) -> int:
-    """Output-tile rows of the bf16 MFMA kernels for an M dimension: 256, or 224 for M = 224k not 256-tiled (the
-    MP / TP8 shard's F/8 = 1792 rows; K-contiguous A layouts only)."""
-    return 256 if M % 256 == 0 else 224
+def use_m224(M: int, N: int) -> bool:
+    """Whether an ``[M, N]`` bf16 GEMM output (K-contiguous A: NT / NN) runs on 224-row tiles: M = 224k and the 224-row
+    grid fills the CUs strictly better than the 256-row one -- e.g. the MP / TP8 shard's F/8 = 1792 rows against
+    T = 8192: 8 x 32 = 256 tiles instead of 7 x 32 = 224 (mirrors csrc/gemm.hip use_m224)."""
+    if M % 224 or N % 256:
+        return False
+    if M % 256:
+        return True
+
+    def fill(bm):
+        t = (M // bm) * (N // 256)
+        return t / (-(-t // NUM_CUS) * NUM_CUS)
+
+    return fill(224) > fill(256)
+
+
+def tile_rows(M: int, N: int) -> int:
+    """Output-tile rows the bf16 MFMA kernels use for an ``[M, N]`` output with a K-contiguous A (224 or 256)."""
+    return 224 if use_m224(M, N) else 256
 
 
 def pair_supported(shapes, dtype: torch.dtype = torch.bfloat16, layout: str = "tn") -> bool:
@@ -367,7 +382,7 @@ def pair_supported(shapes, dtype: torch.dtype = torch.bfloat16, layout: str = "t
     if _VARIANT["name"] not in ("auto", "8phase_stagger"):
         return False
     if layout == "nn":
-        if any(m % 224 or m % 256 == 0 or n % 256 for m, n in ((M0, N0), (M1, N1))):
+        if not (use_m224(M0, N0) and use_m224(M1, N1)):
             return False
         return (M0 // 224) * (N0 // 256) + (M1 // 224) * (N1 // 256) <= NUM_CUS
     if any(m % 256 or n % 256 for m, n in ((M0, N0), (M1, N1))):
@@ -445,14 +460,14 @@ def gemm_pair(a0: torch.Tensor, b0: torch.Tensor, kw0: dict, a1: torch.Tensor, b
 
 def relu_mask_bytes(M: int, N: int) -> int:
     """Size of the ReLU bitmask of an ``[M, N]`` activation (8 KiB per 256x256 or 224x256 tile)."""
-    return (M // tile_rows(M)) * (N // 256) * 8192
+    return (M // tile_rows(M, N)) * (N // 256) * 8192
 
 
 def relu_mask_supported(M: int, N: int, K: int, dtype: torch.dtype = torch.bfloat16) -> bool:
     """Whether the forward (``x·W1ᵀ``, K = D) / dgrad (``dy·W2``, K = D) pair of an ``[M, N]`` ReLU activation runs
     on the 8-phase kernels that share the bitmask's tile-native layout."""
     kstep = 64 if _VARIANT["name"] == "pp" else 128
-    if dtype == torch.bfloat16 and M % 256 and M % 224 == 0 and N % 256 == 0 and K % 128 == 0:
+    if dtype == torch.bfloat16 and use_m224(M, N) and K % 128 == 0:
         return _VARIANT["name"] in ("auto", "8phase_stagger")   # 224-row tiles (transposed-activation TP layout)
     return (dtype == torch.bfloat16 and M % 256 == 0 and N % 256 == 0 and K % kstep == 0
             and choose_ksplit(M, N, K) == 1 and _VARIANT["name"] != "2stage")

@@ -147,11 +147,14 @@ class FFNTrainer:
         if self.sp and T % t:
             raise ValueError("sequence parallelism needs tokens % tp == 0")
         self.T = T
-        # transposed-activation layout (models/ffn.layer_fwd_t): F/tp = 224k not 256-tiled (MP at tp 8: 1792), so the
-        # F-sized GEMM dimensions run on 224-row tiles; activations [F, T], W2 stored as W2ᵀ [F, D]
+        # transposed-activation layout (models/ffn.layer_fwd_t): F/tp = 224k where 224-row tiles fill the chip better
+        # (MP at tp 8: 1792 = 8 x 224 vs 7 x 256), so the F-sized GEMM dimensions run as M on 224-row tiles;
+        # activations [F, T], W2 stored as W2ᵀ [F, D]
+        from ..ops.gemm import use_m224
+
         self.tmode = (cfg.tp_transposed and self.device.type == "cuda" and not self.gated and not self.fsdp
                       and not self.zero and not self.sp and cfg.recompute == "none" and self.cd == torch.bfloat16
-                      and self.F_loc % 256 != 0 and self.F_loc % 224 == 0 and T % 256 == 0 and D % 256 == 0)
+                      and use_m224(self.F_loc, T) and use_m224(self.F_loc, D) and T % 256 == 0)
         self.step_count = 0
         dev = self.device
         if dev.type == "cuda":

@@ -68,7 +68,7 @@ class TrainConfig:
                                      # runs while chunk i+1 computes, and the next layer's chunk i starts as
                                      # soon as that one all-reduce is done (1 = one all-reduce per layer)
     relu_mask: bool = True           # ReLU: the dgrad reads a 1-bit activation mask written by the forward
-    # GPU, F/tp a multiple of 224 but not of 256 (the MP config at tp = 8): keep activations as [F, T] and W2 as W2ᵀ so
+    # GPU, F/tp a multiple of 224 whose 224-row tile grid fills the chip better (the MP config at tp = 8): keep activations as [F, T] and W2 as W2ᵀ so
     # every F-sized GEMM dimension runs on 224-row tiles that fill the chip (models/ffn.layer_fwd_t / layer_bwd_t)
     tp_transposed: bool = True
                                      # GEMM instead of the bf16 activation (GPU, 8-phase kernel shapes)
