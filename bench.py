@@ -514,6 +514,7 @@ def main(argv=None) -> int:
             "peak_hbm_gib": head["peak_hbm_gib"], "state_gib": head["state_gib"], "finite": head["finite"],
             "comm_backend": a.comm, "hip_graph": bool(a.graph), "gemm_variant": a.gemm_variant,
             "tp_allreduce": a.tp_allreduce, "wgrad_stream": head.get("wgrad_stream", False),
+            "pair_wgrads": head.get("pair_wgrads", False), "tp_transposed": head.get("tp_transposed", False),
         }
         for k in ("comm", "phase_ms_per_step", "queues"):
             if k in head:

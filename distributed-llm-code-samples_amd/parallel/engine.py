@@ -256,10 +256,15 @@ class FFNTrainer:
 
         # ---- FSDP rings --------------------------------------------------------------------------
         if self.fsdp:
-            self.wring = [{n: torch.empty(full[n], dtype=self.cd, device=dev) for n in ("w2", "w1")}
-                          for _ in range(2)]
-            self.gring = [{n: torch.empty(full[n], dtype=self.gd, device=dev) for n in ("w2", "w1")}
-                          for _ in range(2)]
+            # dp = 1 (forced communicators on one device): a rank's shard IS the full weight, so the gathers read and
+            # write the working copy in place and the gradient GEMMs write the shard gradient directly -- size-1
+            # collectives that move nothing (RCCL launches no kernel), the degenerate case of the N-rank schedule
+            # (every wait, event and stream edge is still issued).  dp > 1: 2-slot gather / gradient rings.
+            self.fsdp_alias = d == 1
+            self.wring = [{n: torch.empty(0 if self.fsdp_alias else full[n], dtype=self.cd, device=dev)
+                           for n in ("w2", "w1")} for _ in range(2)]
+            self.gring = [{n: torch.empty(0 if self.fsdp_alias else full[n], dtype=self.gd, device=dev)
+                           for n in ("w2", "w1")} for _ in range(2)]
             self.ag_work = [None, None]     # per slot: {name: work} of the in-flight gather (None: landed)
             self.ag_layer = [-1, -1]
             self.rs_pending = [None, None]  # per slot: (layer, {name: work}) -- one reduce-scatter per weight
@@ -373,7 +378,10 @@ class FFNTrainer:
             self.opt_stream = self._side_stream("opt")
             self.ddp_done = [None] * len(self.buckets)
         if self.zero:
-            self.gshard = torch.zeros(self.shard_total, dtype=self.gd, device=dev)
+            # dp = 1: the owned shard of every bucket is the whole bucket, so the reduced gradient IS the gradient
+            # buffer (in-place size-1 reduce-scatter, no copy)
+            self.gshard = (self.grads[:self.shard_total] if d == 1 else
+                           torch.zeros(self.shard_total, dtype=self.gd, device=dev))
             self.ag_pending = [None] * len(self.buckets)
             self.rs_issued_at = [None] * len(self.buckets)
         self._next_bucket = 0
@@ -754,7 +762,7 @@ class FFNTrainer:
             # one reduce-scatter per weight, issued the moment its gradient GEMM is done: the first weight's
             # collective runs under the layer's remaining GEMMs instead of waiting for both
             slot = l % 2
-            w = comm.reduce_scatter_into(self.grad_view(l, name), self.gring[slot][name], self.mesh.group("dp_rs"),
+            w = comm.reduce_scatter_into(self.grad_view(l, name), self._fsdp_gbuf(l, name), self.mesh.group("dp_rs"),
                                          async_op=True)
             if self.rs_pending[slot] is None or self.rs_pending[slot][0] != l:
                 self.rs_pending[slot] = (l, {})
@@ -866,7 +874,7 @@ class FFNTrainer:
         if self.ag_layer[slot] != l or self.ag_work[slot] is None:
             self.ag_work[slot] = {}
         # the weights' shard all-gathers as one group (native: one fused RCCL launch)
-        w = comm.all_gather_into_many([(self.wring[slot][n], self.copy_view(l, n)) for n in names], grp,
+        w = comm.all_gather_into_many([(self._fsdp_wbuf(l, n), self.copy_view(l, n)) for n in names], grp,
                                       async_op=True)
         for n in names:
             self.ag_work[slot][n] = w
@@ -880,7 +888,15 @@ class FFNTrainer:
         works = self.ag_work[slot]
         if works is not None and works.get(name) is not None:
             works.pop(name).wait()
-        return self.wring[slot][name]
+        return self._fsdp_wbuf(l, name)
+
+    def _fsdp_wbuf(self, l: int, name: str) -> torch.Tensor:
+        """Where layer l's gathered weight lives: its ring slot, or (dp = 1) the working copy itself."""
+        return self.copy_view(l, name) if self.fsdp_alias else self.wring[l % 2][name]
+
+    def _fsdp_gbuf(self, l: int, name: str) -> torch.Tensor:
+        """Where layer l's full weight gradient is written: its ring slot, or (dp = 1) the shard gradient itself."""
+        return self.grad_view(l, name) if self.fsdp_alias else self.gring[l % 2][name]
 
     def _fsdp_weights(self, l: int) -> tuple[torch.Tensor, torch.Tensor]:
         return self._fsdp_weight(l, "w1"), self._fsdp_weight(l, "w2")
@@ -947,7 +963,7 @@ class FFNTrainer:
         for l in range(L):
             if self.fsdp:
                 w1 = self._fsdp_weight(l, "w1")   # W2 is waited for right before the second GEMM
-                w2 = self.wring[l % 2]["w2"]
+                w2 = self._fsdp_wbuf(l, "w2")
                 self.ag_next.discard(l)
                 if l + 1 < L and (l + 1) not in self.ag_next:
                     self._fsdp_gather(l + 1)
@@ -1036,7 +1052,7 @@ class FFNTrainer:
                     w1, w2 = self._fsdp_weights(l)
                 slot = l % 2
                 self._fsdp_finish_rs_side(slot)  # slot's previous grads (layer l+2) must be reduced first
-                gw1, gw2 = self.gring[slot]["w1"], self.gring[slot]["w2"]
+                gw1, gw2 = self._fsdp_gbuf(l, "w1"), self._fsdp_gbuf(l, "w2")
             elif self.fused_opt:
                 w1, w2 = self.copy_view(l, "w1"), self.copy_view(l, "w2")
                 gw1, gw2 = self._fused_wgrad_kw(l, "w1"), self._fused_wgrad_kw(l, "w2")

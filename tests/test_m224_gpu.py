@@ -9,7 +9,7 @@ the regular one (reference: the TP worker, train_ffns.py:290-312)."""
 import pytest
 import torch
 
-from dllm.ops.gemm import gemm, gemm_pair, gemm_path, relu_mask_bytes
+from dllm.ops.gemm import gemm, gemm_pair, gemm_path, relu_mask_bytes, set_splitk
 from dllm.ops.master import join_master, split_master
 
 pytestmark = pytest.mark.gpu
@@ -42,7 +42,11 @@ def test_m224_equals_padded_256(layout, epi, out_dtype):
     out = torch.empty(M, N, dtype=out_dtype, device=DEV)
     gemm(a, b, layout, out=out, **kw)
     ref = torch.empty(2048, N, dtype=out_dtype, device=DEV)
-    gemm(_pad_rows(a), b, layout, out=ref, **kw)
+    old = set_splitk(False)   # the reference: whole 256-row tiles, same per-element K order (no split-K partials)
+    try:
+        gemm(_pad_rows(a), b, layout, out=ref, **kw)
+    finally:
+        set_splitk(old)
     torch.cuda.synchronize()
     assert torch.equal(out, ref[:M])
     exact = a.double() @ (b.double().t() if layout == "nt" else b.double())
