@@ -88,3 +88,22 @@ def test_bench_self_launch_propagates_rank_failure():
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
     assert r.returncode != 0
     assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+def test_bench_self_launch_four_ranks_all_methods():
+    """The driver's plain ``python bench.py --gpus 4`` shape: four self-launched ranks, every side method on its own
+    mesh (hybrid = FSDP 2 x TP 2), communicator sizes reported per method, the differential exposed-comm field present."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--steps", "1", "--warmup", "1",
+           "--backend", "gloo", "--model_size", "64", "--layers", "2", "--batch_size", "2", "--seq_len", "16",
+           "--dtype", "fp32", "--mp_ffn_dim", "128", "--llama_ffn_dim", "128", "--llama_layers", "2",
+           "--method_steps", "1", "--diff_pairs", "1", "--diff_steps", "1", "--observe_steps", "0"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["PYTHONPATH"] = ROOT
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert rec["world_size"] == 4 and rec["config"]["parallelism"] == "dp4-zero2"
+    m = rec["methods"]
+    assert m["hybrid"]["parallelism"] == "fsdp2xtp2" and m["hybrid"]["comm_sizes"]["tp"] == 2
+    assert m["hybrid"]["comm_sizes"]["dp_rs"] == 2 and m["tp"]["comm_sizes"] == {"tp": 4}
+    assert all("exposed_ms_diff" in m[k]["comm"] for k in ("ddp", "zero", "fsdp", "hybrid"))
