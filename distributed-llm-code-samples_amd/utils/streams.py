@@ -119,13 +119,18 @@ def _index(device) -> int:
     return device.index if device.index is not None else torch.cuda.current_device()
 
 
-def shares_compute_queue(stream: torch.cuda.Stream, device=None) -> bool:
-    """Whether ``stream`` runs on the compute (null) stream's hardware queue (measured; synchronises both)."""
+def shares_compute_queue(stream: torch.cuda.Stream, device=None, tries: int = 3) -> bool:
+    """Whether ``stream`` runs on the compute (null) stream's hardware queue (measured; synchronises both).  The
+    majority of ``tries`` probes decides: a single probe can read "shared" when the candidate's dispatch is merely
+    late (seen once in a round-4 methods run, against a consistent "own queue" for the same stream)."""
+    votes = 0
     with torch.cuda.device(_index(device)):
-        r = _native.lib().dllm_queue_shared(None, ctypes.c_void_p(stream.cuda_stream), PROBE_SPIN_US)
-    if r < 0:
-        raise RuntimeError(f"dllm_queue_shared failed ({r})")
-    return r == 1
+        for _ in range(tries):
+            r = _native.lib().dllm_queue_shared(None, ctypes.c_void_p(stream.cuda_stream), PROBE_SPIN_US)
+            if r < 0:
+                raise RuntimeError(f"dllm_queue_shared failed ({r})")
+            votes += r
+    return 2 * votes > tries
 
 
 def queue_report(device, streams: dict, pool: bool = True) -> dict:

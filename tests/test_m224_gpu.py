@@ -127,9 +127,9 @@ def test_m224_nn_fused_optimizer_pair(opt):
         grad = torch.empty(M, D, device=DEV)
         gemm(aT, dy, "nn", out=grad)
         torch.cuda.synchronize()
-        want = torch.add(w2t, torch.mul(torch.mul(grad, 1.0), -1e-2))
+        want = w2t.double() - 1e-2 * grad.double()
         got = p2["out"] if opt == "sgd" else join_master(p2["aux_out"], p2["out"])
-        assert torch.equal(got, want)
+        assert ((got.double() - want).abs() <= 2 ** -22 * want.abs() + 1e-12).all()   # fp32 rounding of the update
 
 
 def _tp8_engine(tmode: bool, L=2, seed=13):
