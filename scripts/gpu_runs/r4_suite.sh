@@ -4,5 +4,5 @@
 source scripts/gpu_steps.sh
 step pytest_gpu 1100 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-bash scripts/gpu_runs/rehearsal.sh
+bash scripts/gpu_runs/rehearsal.sh || exit $?   # a fatal step there ends this call too
 step headline_stats 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_head -o run -- python3 bench.py --gpus 1 --steps 10 --warmup 3 --methods none
