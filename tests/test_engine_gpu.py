@@ -244,19 +244,25 @@ def test_wgrad_stream_bitwise(act, gated):
     """Weight-gradient GEMMs on a concurrent stream == the sequential schedule, bitwise (same kernels and
     inputs per GEMM; the stream/event edges order every weight update after its last reader); gated (SwiGLU)
     stacks run the DGLU dgrad on the main stream."""
+    from dllm.ops.gemm import set_pair_wgrads
+
     D, F, L, T, lr = 512, 2048, 4, 1024, 1e-2
     layers, batches = _setup(D, F, L, T, act, gated, 3)
     outs = []
-    for ws in (False, True):
-        cfg = TrainConfig(model=ModelConfig(D, F, L, act, gated), batch_size=1, seq_len=T, dtype="bf16",
-                          grad_dtype="fp32", lr=lr, wgrad_stream=ws)
-        eng = FFNTrainer(cfg, Mesh(), torch.device("cuda"))
-        assert (eng.wg_stream is not None) == ws
-        eng.load_full_params(layers)
-        for x, dy in batches:
-            eng.train_step(x.cuda().bfloat16(), dy.cuda().bfloat16())
-        torch.cuda.synchronize()
-        outs.append(eng.master.clone())
+    old_pair = set_pair_wgrads(False)   # these small weight gradients would otherwise run as one grouped launch
+    try:
+        for ws in (False, True):
+            cfg = TrainConfig(model=ModelConfig(D, F, L, act, gated), batch_size=1, seq_len=T, dtype="bf16",
+                              grad_dtype="fp32", lr=lr, wgrad_stream=ws)
+            eng = FFNTrainer(cfg, Mesh(), torch.device("cuda"))
+            assert (eng.wg_stream is not None) == ws
+            eng.load_full_params(layers)
+            for x, dy in batches:
+                eng.train_step(x.cuda().bfloat16(), dy.cuda().bfloat16())
+            torch.cuda.synchronize()
+            outs.append(eng.master.clone())
+    finally:
+        set_pair_wgrads(old_pair)
     assert torch.equal(outs[0], outs[1])
 
 

@@ -125,7 +125,7 @@ def test_engine_tp8_shard_pairs_wgrads():
         old = set_pair_wgrads(paired)
         try:
             cfg = TrainConfig(model=ModelConfig(4096, 1792, 2, "relu", False), batch_size=2, seq_len=1024,
-                              dtype="bf16", grad_dtype="bf16", wgrad_stream=False)
+                              dtype="bf16", grad_dtype="bf16", wgrad_stream=False, tp_transposed=False)
             eng = FFNTrainer(cfg, Mesh(), torch.device("cuda"))
             assert eng.pair_wgrads == paired
             eng.load_full_params(init_ffn_params_device(4096, 1792, 2, 9, torch.device("cuda"), False))

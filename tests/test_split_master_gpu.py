@@ -173,6 +173,7 @@ def test_engine_high_priority_side_streams_bitwise(monkeypatch):
     layers = [{"w1": torch.randn(F, D, generator=g) * 0.02, "w2": torch.randn(D, F, generator=g) * 0.02}
               for _ in range(L)]
     outs = []
+    monkeypatch.setattr("dllm.ops.gemm._PAIR", {"enabled": False})  # keep the weight-gradient stream in use
     for mode in ("pool", "high", "auto"):
         monkeypatch.setenv("DLLM_SIDE_STREAMS", mode)
         cfg = TrainConfig(model=ModelConfig(D, F, L), batch_size=2, seq_len=512, dtype="bf16", grad_dtype="bf16",
