@@ -16,10 +16,14 @@
 
 namespace dllm {
 
+// rounds of the mock-data Philox (build-time: 10 = Random123's default Philox4x32-10)
+#ifndef DLLM_PHILOX_ROUNDS
+#define DLLM_PHILOX_ROUNDS 10
+#endif
 __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
   const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
 #pragma unroll
-  for (int r = 0; r < 10; ++r) {
+  for (int r = 0; r < DLLM_PHILOX_ROUNDS; ++r) {
     // one 32x32->64 multiply per product (v_mad_u64_u32) instead of separate mul_lo / mul_hi
     const uint64_t p0 = (uint64_t)M0 * c.x, p1 = (uint64_t)M1 * c.z;
     const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
