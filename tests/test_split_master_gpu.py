@@ -6,6 +6,8 @@ optimizer kernel -- must leave bitwise the fp32 master the fp32-master form leav
 that master rounded half away from zero.  The engine check: one training step from bf16-representable weights (no
 rounding ties at the start) gives bitwise the fp32-master engine's master.
 """
+import sys
+
 import pytest
 import torch
 
@@ -173,7 +175,8 @@ def test_engine_high_priority_side_streams_bitwise(monkeypatch):
     layers = [{"w1": torch.randn(F, D, generator=g) * 0.02, "w2": torch.randn(D, F, generator=g) * 0.02}
               for _ in range(L)]
     outs = []
-    monkeypatch.setattr("dllm.ops.gemm._PAIR", {"enabled": False})  # keep the weight-gradient stream in use
+    # keep the weight-gradient stream in use (dllm.ops re-exports a function named gemm: patch the module itself)
+    monkeypatch.setitem(sys.modules["dllm.ops.gemm"]._PAIR, "enabled", False)
     for mode in ("pool", "high", "auto"):
         monkeypatch.setenv("DLLM_SIDE_STREAMS", mode)
         cfg = TrainConfig(model=ModelConfig(D, F, L), batch_size=2, seq_len=512, dtype="bf16", grad_dtype="bf16",
