@@ -1029,17 +1029,6 @@ __device__ __forceinline__ void gemm_8ph_body(const GemmArgs& p, const int which
   // A separate instantiation, so the one-tile-per-block kernels carry none of its state.
   const bool pers = PERS && !GRP && NPH == 8 && p.tpb > 1;
   int slot = slot0;
-#ifdef DLLM_XCD_SKEW_US
-  // experiment knob (build-time): blocks on odd XCDs (dispatch is round-robin over the 8 XCDs) start the fused-SGD
-  // weight gradient this many microseconds late, so the two XCD halves reach their epilogue bursts at different times
-  // while every XCD's blocks stay in K lockstep among themselves (each XCD has its own L2)
-  if constexpr (EPI == EPI_SGDS && PERS) {
-    if (blockIdx.x & 1) {
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)(DLLM_XCD_SKEW_US * 100)) __builtin_amdgcn_s_sleep(2);
-    }
-  }
-#endif
   // Per-slot helpers take the argument block explicitly: inside the slot loop they are called with a fresh
   // reload_args() copy, so the epilogue's arguments are loaded where they are used instead of being kept
   // live in SGPRs across the whole main loop.

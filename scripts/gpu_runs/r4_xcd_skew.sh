@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 4 experiment: the fused split-master SGD weight-gradient epilogue with half the XCDs starting late
+# Round 4 experiment (knob since removed; result in profiles/r4/xcd_skew_sgd_epilogue_r4.txt): the fused split-master SGD weight-gradient epilogue with half the XCDs starting late
 # (build knob DLLM_XCD_SKEW_US: _dllm_native_skew15.so / _skew30.so through DLLM_NATIVE_LIB), isolated GEMM and the
 # headline step, interleaved with the default build.
 source scripts/gpu_steps.sh
