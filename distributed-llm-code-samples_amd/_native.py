@@ -22,8 +22,8 @@ _ERR: str | None = None
 
 c_int, c_long, c_float, c_void_p, c_ull = ctypes.c_int, ctypes.c_long, ctypes.c_float, ctypes.c_void_p, ctypes.c_ulonglong
 
-# bumped with every signature change below (csrc/elementwise.hip dllm_abi_version): a stale library fails loudly
-ABI_VERSION = 10
+# bumped with every signature or stream-semantics change below (csrc/elementwise.hip dllm_abi_version): a stale library fails loudly
+ABI_VERSION = 11
 
 _SIGS = {
     "dllm_gemm": (c_int, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_long, c_void_p, c_long, c_void_p, c_long,

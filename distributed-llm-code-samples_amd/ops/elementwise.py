@@ -16,6 +16,8 @@ def rng_normal_(out: torch.Tensor, seed: int, stream_id: int = 0, scale: float =
 
     GPU: Philox4x32-10 kernel.  CPU: the same Philox stream computed in torch (bitwise-identical
     uniform draws; normals equal up to libm differences), so CPU tests and GPU runs see the same data.
+    fp32 outputs take 32-bit uniforms (4 normals per Philox call); bf16 outputs, which keep 8 mantissa bits, take
+    16-bit uniforms (8 normals per call, csrc/elementwise.hip ``rng_normal_bf16_kernel``).
     """
     if not out.is_contiguous():
         raise ValueError("rng_normal_ needs a contiguous tensor")
@@ -25,7 +27,7 @@ def rng_normal_(out: torch.Tensor, seed: int, stream_id: int = 0, scale: float =
                                            stream_id & (2**64 - 1), float(scale), _native.stream_ptr(out.device))
         _native.check(rc, "dllm_rng_normal")
         return out
-    out.copy_(_philox_normal_cpu(n, seed, stream_id, scale).view(out.shape))
+    out.copy_(_philox_normal_cpu(n, seed, stream_id, scale, u16=out.dtype == torch.bfloat16).view(out.shape))
     return out
 
 
@@ -63,8 +65,11 @@ def philox4x32_10(c0, c1, c2, c3, k0: int, k1: int):
     return c0, c1, c2, c3
 
 
-def _philox_normal_cpu(n: int, seed: int, stream_id: int, scale: float) -> torch.Tensor:
-    n4 = (n + 3) // 4
+def _philox_normal_cpu(n: int, seed: int, stream_id: int, scale: float, u16: bool = False) -> torch.Tensor:
+    """``u16``: the bf16 stream -- counter i yields outputs 8i..8i+7 from Box-Muller pairs (lo16, hi16) of its four
+    words, u1 = 1 - a/2^16 in (0, 1], u2 = b/2^16 in [0, 1)."""
+    per = 8 if u16 else 4
+    n4 = (n + per - 1) // per
     idx = torch.arange(n4, dtype=torch.int64)
     c0, c1, c2, c3 = philox4x32_10(idx & 0xFFFFFFFF, (idx >> 32) & 0xFFFFFFFF,
                                    torch.full_like(idx, stream_id & 0xFFFFFFFF),
@@ -79,6 +84,14 @@ def _philox_normal_cpu(n: int, seed: int, stream_id: int, scale: float) -> torch
         th = 2 * math.pi * u2
         return r * torch.cos(th), r * torch.sin(th)
 
+    if u16:
+        zs = []
+        for c in (c0, c1, c2, c3):
+            u1 = 1.0 - (c & 0xFFFF).to(torch.float32) * 2.0 ** -16
+            th = 2 * math.pi * ((c >> 16) & 0xFFFF).to(torch.float32) * 2.0 ** -16
+            r = torch.sqrt(-2.0 * torch.log(u1)) * scale
+            zs += [r * torch.cos(th), r * torch.sin(th)]
+        return torch.stack(zs, dim=1).reshape(-1)[:n]
     z0, z1 = bm(c0, c1)
     z2, z3 = bm(c2, c3)
     z = torch.stack([z0, z1, z2, z3], dim=1).reshape(-1)[:n]

@@ -30,6 +30,27 @@ def test_rng_deterministic_and_normal():
     assert abs(z.mean().item()) < 1e-2 and abs(z.std().item() - 1.0) < 1e-2
 
 
+def test_rng_bf16_stream_16bit_uniforms():
+    """bf16 draws: 8 normals per Philox call from 16-bit uniforms (u1 = 1 - lo16/2^16, u2 = hi16/2^16), a prefix of a
+    longer draw, N(0, 1) moments and tail mass, radius bounded by sqrt(-2 ln 2^-16)."""
+    import math
+
+    z = _philox_normal_cpu(1 << 20, 11, 0, 1.0, u16=True)
+    assert abs(z.mean().item()) < 5e-3 and abs(z.std().item() - 1.0) < 5e-3
+    assert abs((z.abs() > 2).float().mean().item() - 0.0455) < 2e-3
+    assert z.abs().max().item() <= math.sqrt(-2 * math.log(2.0 ** -16)) + 1e-4
+    c0, _, _, _ = philox4x32_10(torch.zeros(1, dtype=torch.int64), torch.zeros(1, dtype=torch.int64),
+                                torch.zeros(1, dtype=torch.int64), torch.zeros(1, dtype=torch.int64), 11, 0)
+    w = int(c0[0])
+    u1, u2 = 1.0 - (w & 0xFFFF) / 65536.0, (w >> 16) / 65536.0
+    assert abs(z[0].item() - math.sqrt(-2 * math.log(u1)) * math.cos(2 * math.pi * u2)) < 1e-5
+    a = torch.empty(13, dtype=torch.bfloat16)
+    b = torch.empty(1000, dtype=torch.bfloat16)
+    rng_normal_(a, seed=5, stream_id=1)
+    rng_normal_(b, seed=5, stream_id=1)
+    assert torch.equal(a, b[:13])
+
+
 def test_gemm_layouts_cpu():
     a, b = torch.randn(6, 5), torch.randn(7, 5)
     torch.testing.assert_close(gemm(a, b, "nt"), a @ b.t())
