@@ -222,6 +222,9 @@ def parse(argv=None):
                    help="communicating methods: interleaved pairs of (--diff_steps normal steps, --diff_steps steps with "
                         "every collective elided); exposed_ms_diff = median normal - median elided step time")
     p.add_argument("--diff_steps", type=int, default=4)
+    p.add_argument("--elide_collectives", action="store_true",
+                   help="diagnostic (not a valid measurement of the method): run every step with the collectives "
+                        "elided, as the exposed_ms_diff reference steps do, e.g. to kernel-trace both variants")
     p.add_argument("--no_pair_wgrads", action="store_true",
                    help="run small-grid weight-gradient pairs (the MP / TP8 shard) as two split-K GEMMs instead of one "
                         "grouped launch")
@@ -332,11 +335,16 @@ def _run_on_mesh(a, method, cfg, mesh, n, world, dev, steps, warmup, force_comm,
         eng.before_backward = data.release
 
     def one_step(seed):
-        if graphed is not None:
-            graphed.step(seed)
-        else:
-            x, dy = data.fill(seed, next_seed=seed + 1)
-            eng.train_step(x, dy)
+        old = comm.set_elide(True) if a.elide_collectives else None
+        try:
+            if graphed is not None:
+                graphed.step(seed)
+            else:
+                x, dy = data.fill(seed, next_seed=seed + 1)
+                eng.train_step(x, dy)
+        finally:
+            if old is not None:
+                comm.set_elide(old)
 
     for i in range(warmup):
         one_step(seed_base + i)
@@ -380,6 +388,8 @@ def _run_on_mesh(a, method, cfg, mesh, n, world, dev, steps, warmup, force_comm,
            "pair_wgrads": bool(eng.pair_wgrads), "tp_transposed": bool(eng.tmode),
            # the ranks each role communicator actually spans (RCCL / gloo group sizes; {} = no collective)
            "comm_sizes": {role: g.size() for role, g in mesh.groups.items() if g is not None}}
+    if a.elide_collectives:
+        rec["collectives_elided"] = True   # diagnostic run: not the method's step time
     if phases:
         rec["phase_ms_per_step"] = phases
     if queues is not None:
@@ -394,7 +404,7 @@ def _run_on_mesh(a, method, cfg, mesh, n, world, dev, steps, warmup, force_comm,
                 one_step(nxt + i)
         nxt += observe_steps
         rec["comm"] = obs.summary(observe_steps)
-    if a.diff_pairs > 0 and a.diff_steps > 0 and communicates and graphed is None:
+    if a.diff_pairs > 0 and a.diff_steps > 0 and communicates and graphed is None and not a.elide_collectives:
         # differential exposed communication: the same engine with its collectives elided (compute only), interleaved
         # with normal steps in this process; the difference of the medians is the step time the collectives add
         on, off = [], []
@@ -516,7 +526,7 @@ def main(argv=None) -> int:
             "tp_allreduce": a.tp_allreduce, "wgrad_stream": head.get("wgrad_stream", False),
             "pair_wgrads": head.get("pair_wgrads", False), "tp_transposed": head.get("tp_transposed", False),
         }
-        for k in ("comm", "phase_ms_per_step", "queues"):
+        for k in ("comm", "phase_ms_per_step", "queues", "collectives_elided"):
             if k in head:
                 rec[k] = head[k]
         if side:
