@@ -32,15 +32,37 @@ class Done:
         return True
 
 
+class Elided:
+    """An infinitely fast collective (``set_elide``): issued on the current stream, ``wait()`` orders the waiting
+    stream after that issue point.  The step keeps every data dependency a real collective carries (e.g. the next
+    forward still waits for the shard update whose result the all-gather would ship); only the transfer and the
+    collective stream's hops are gone."""
+
+    def __init__(self, t: torch.Tensor):
+        self.ev = None
+        if t.is_cuda:
+            self.ev = torch.cuda.Event()
+            self.ev.record(torch.cuda.current_stream(t.device))
+        self.device = t.device
+
+    def wait(self):
+        if self.ev is not None:
+            torch.cuda.current_stream(self.device).wait_event(self.ev)
+        return True
+
+    def is_completed(self):
+        return self.ev is None or self.ev.query()
+
+
 _SERIALIZE = False
 _ELIDE = False
 
 
 def set_elide(flag: bool) -> bool:
     """Timing mode for the differential exposed-communication measurement (bench.py ``exposed_ms_diff``): every
-    collective on a communicator returns at once without running, so a step costs its compute alone.  The results of
-    such steps are meaningless (gradients are not reduced, shards not gathered); only their time is used.  Returns
-    the previous setting."""
+    collective on a communicator returns an ``Elided`` handle at once without running, so a step costs its compute
+    and its dependency edges alone.  The results of such steps are meaningless (gradients are not reduced, shards
+    not gathered); only their time is used.  Returns the previous setting."""
     global _ELIDE
     old, _ELIDE = _ELIDE, bool(flag)
     return old
@@ -128,7 +150,7 @@ def _issue(group, fn, moves: bool = True):
 
 def all_reduce(t: torch.Tensor, group, async_op: bool = True):
     if _ELIDE and group is not None:
-        return Done()
+        return Elided(t)
     if group is not None and _native(group):
         w = _issue(group, lambda: group.all_reduce(t), _moves(group, t, t))
         return _finish(w, async_op) if (async_op or _SERIALIZE) else (w.wait(), Done())[1]
@@ -141,7 +163,7 @@ def all_reduce(t: torch.Tensor, group, async_op: bool = True):
 
 def all_gather_into(out: torch.Tensor, shard: torch.Tensor, group, async_op: bool = True):
     if _ELIDE and group is not None:
-        return Done()
+        return Elided(out)
     if group is not None and _native(group):
         w = _issue(group, lambda: group.all_gather_into(out.view(-1), shard.reshape(-1)), _moves(group, out, shard))
         return _finish(w, async_op) if (async_op or _SERIALIZE) else (w.wait(), Done())[1]
@@ -159,7 +181,7 @@ def all_gather_into(out: torch.Tensor, shard: torch.Tensor, group, async_op: boo
 
 def reduce_scatter_into(out: torch.Tensor, full: torch.Tensor, group, async_op: bool = True):
     if _ELIDE and group is not None:
-        return Done()
+        return Elided(out)
     if group is not None and _native(group):
         w = _issue(group, lambda: group.reduce_scatter_into(out.view(-1), full.reshape(-1)), _moves(group, out, full))
         return _finish(w, async_op) if (async_op or _SERIALIZE) else (w.wait(), Done())[1]
@@ -194,7 +216,7 @@ def all_gather_into_many(pairs, group, async_op: bool = True):
     """All-gathers ``(out, shard)`` issued as ONE group: the native layer fuses them with
     ncclGroupStart/End (one launch, one completion event); torch / gloo issue them back to back."""
     if _ELIDE and group is not None:
-        return Done()
+        return Elided(pairs[0][0])
     if group is not None and _native(group) and not _SERIALIZE:
         w = _issue(group, lambda: group.all_gather_into_many([(o.view(-1), sh.reshape(-1)) for o, sh in pairs]),
                    any(_moves(group, o, sh) for o, sh in pairs))
@@ -206,7 +228,7 @@ def all_gather_into_many(pairs, group, async_op: bool = True):
 def reduce_scatter_into_many(pairs, group, async_op: bool = True):
     """Reduce-scatters ``(out, full)`` issued as ONE group (see ``all_gather_into_many``)."""
     if _ELIDE and group is not None:
-        return Done()
+        return Elided(pairs[0][0])
     if group is not None and _native(group) and not _SERIALIZE:
         w = _issue(group, lambda: group.reduce_scatter_into_many([(o.view(-1), f.reshape(-1)) for o, f in pairs]),
                    any(_moves(group, o, f) for o, f in pairs))

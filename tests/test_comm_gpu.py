@@ -145,3 +145,30 @@ def test_native_single_process_rccl_selftest():
     assert "PASSED" in r.stdout
     for op in ("all_gather ok", "all_reduce ok", "reduce_scatter ok"):
         assert op in r.stdout
+
+
+def test_elided_collective_keeps_dependency(pg):
+    """exposed_ms_diff's reference steps: an elided collective returns at once but its wait() still orders the waiting
+    stream after the issue point (the producer's kernels), like an infinitely fast collective."""
+    from dllm.ops.elementwise import occupy_cus
+    from dllm.parallel import comm
+
+    dev = torch.device("cuda", 0)
+    mesh = Mesh.build(1, 1, force=True, comm_backend="torch", device=dev)
+    x = torch.zeros(1 << 20, device=dev)
+    side = torch.cuda.Stream(device=dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    old = comm.set_elide(True)
+    try:
+        with torch.cuda.stream(side):
+            occupy_cus(8, 3000.0, device=dev)   # 3 ms on the producer stream before the write
+            x.fill_(1.0)
+            w = comm.all_gather_into(x, x, mesh.group("dp_ag"), async_op=True)
+        assert isinstance(w, comm.Elided)
+        w.wait()
+        y = x * 2.0
+    finally:
+        comm.set_elide(old)
+    torch.cuda.synchronize()
+    assert torch.all(y == 2.0)
+    mesh.destroy()
