@@ -107,3 +107,27 @@ def test_bench_self_launch_four_ranks_all_methods():
     assert m["hybrid"]["parallelism"] == "fsdp2xtp2" and m["hybrid"]["comm_sizes"]["tp"] == 2
     assert m["hybrid"]["comm_sizes"]["dp_rs"] == 2 and m["tp"]["comm_sizes"] == {"tp": 4}
     assert all("exposed_ms_diff" in m[k]["comm"] for k in ("ddp", "zero", "fsdp", "hybrid"))
+
+
+def test_bench_self_launch_eight_ranks_all_methods():
+    """The driver's largest shape, ``python bench.py --gpus 8`` with no launcher, rehearsed over gloo on the CPU: eight
+    self-launched ranks, headline ZeRO-2 over 8, MP over 8, hybrid FSDP 4 x TP 2, every role communicator sized as
+    RCCL would see it."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--steps", "1", "--warmup", "1",
+           "--backend", "gloo", "--model_size", "64", "--layers", "2", "--batch_size", "1", "--seq_len", "16",
+           "--dtype", "fp32", "--mp_ffn_dim", "256", "--llama_ffn_dim", "128", "--llama_layers", "2",
+           "--method_steps", "1", "--diff_pairs", "1", "--diff_steps", "1", "--observe_steps", "0"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["PYTHONPATH"] = ROOT
+    env["OMP_NUM_THREADS"] = "1"
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=1200, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1   # rank 0 alone prints
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 8 and rec["world_size"] == 8 and rec["launcher"] == "self"
+    assert rec["config"]["parallelism"] == "dp8-zero2" and rec["comm_sizes"]["dp_rs"] == 8
+    m = rec["methods"]
+    assert m["tp"]["comm_sizes"] == {"tp": 8}
+    assert m["hybrid"]["parallelism"] == "fsdp4xtp2" and m["hybrid"]["comm_sizes"]["dp_ag"] == 4
+    assert all(m[k]["finite"] for k in m)
