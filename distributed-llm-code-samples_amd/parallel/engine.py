@@ -164,8 +164,11 @@ class FFNTrainer:
             # (profiles/r3/gated_llama_dims_tpb_wgs_r3.txt)
             set_tiles_per_block(cfg.gemm_tiles_per_block or 8)
             set_fp32_mode(cfg.fp32_gemm)
-            # collectives overlapping the GEMMs (any multi-rank mesh, or forced size-1 communicators)
-            set_min_blocks_per_cu(cfg.gemm_min_bpc or (2 if (mesh.world > 1 or cfg.force_comm) else 1))
+            # collectives overlapping the GEMMs on a multi-rank mesh: RCCL kernels take CU slots, so keep >= 2 blocks
+            # per CU.  Forced size-1 communicators launch no collective kernel (in place, nothing to move) and run
+            # with one: hybrid 172.2-172.4 vs 175.8-176.1 ms, zero 30.5-30.7 vs 30.9-31.0
+            # (profiles/r4/min_bpc_forcecomm_r4.txt)
+            set_min_blocks_per_cu(cfg.gemm_min_bpc or (2 if mesh.world > 1 else 1))
         if cfg.debug_sync:
             comm.set_serialize(True)
         # custom xGMI all-reduce for the TP activation exchange (opt-in; gradients stay on RCCL)
