@@ -16,6 +16,8 @@ no-op returning an already-completed handle.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -56,6 +58,9 @@ class Elided:
 
 _SERIALIZE = False
 _ELIDE = False
+# synchronous collectives on the caller's stream (all_reduce); DLLM_SYNC_INLINE=0 routes them through the
+# communicator stream as before (A/B)
+_SYNC_INLINE = os.environ.get("DLLM_SYNC_INLINE", "1") != "0"
 
 
 def set_elide(flag: bool) -> bool:
@@ -149,12 +154,24 @@ def _issue(group, fn, moves: bool = True):
 
 
 def all_reduce(t: torch.Tensor, group, async_op: bool = True):
+    """``async_op=False`` (a consumer right behind it, e.g. the TP forward's output exchange): the collective is
+    enqueued on the caller's current stream -- native: ``NativeGroup.all_reduce_inline``; torch: ProcessGroupNCCL
+    launches synchronous collectives on the current stream -- so it costs no event hops to a communicator stream and
+    back, each a cross-queue wait (``profiles/r4/forced_comm_gaps_r4.txt``).  Under a ``CommObserver`` it stays on
+    the communicator stream, where the observer times it."""
     if _ELIDE and group is not None:
         return Elided(t)
+    inline = not async_op and not _SERIALIZE and observe.active() is None and _SYNC_INLINE
     if group is not None and _native(group):
+        if inline:
+            _issue(group, lambda: group.all_reduce_inline(t))
+            return Done()
         w = _issue(group, lambda: group.all_reduce(t), _moves(group, t, t))
         return _finish(w, async_op) if (async_op or _SERIALIZE) else (w.wait(), Done())[1]
     if not _active(group):
+        return Done()
+    if inline:
+        _issue(group, lambda: dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=False))
         return Done()
     w = _issue(group, lambda: dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=True),
                _moves(group, t, t))

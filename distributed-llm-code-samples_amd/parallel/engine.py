@@ -1016,11 +1016,13 @@ class FFNTrainer:
                     layer_fwd(self.xs[l], w1, w2, act, gated, a, h, self.xs[l + 1], before_fwd2=before2,
                               mask=self._mask(l))
                 if self.tp_comm:
+                    last = l == L - 1
                     if self.tp_car is not None:
                         w = self.tp_car.all_reduce_async(self.xs[l + 1])
                     else:
-                        w = comm.all_reduce(self.xs[l + 1], tpg, async_op=True)
-                    if l == L - 1:
+                        # the next layer reads it at once: synchronous, on the compute stream (no stream hops)
+                        w = comm.all_reduce(self.xs[l + 1], tpg, async_op=last)
+                    if last:
                         self._tp_pending = [w]
                     else:
                         w.wait()

@@ -188,6 +188,13 @@ class NativeGroup:
 
         return self._enqueue(run, (t,))
 
+    def all_reduce_inline(self, t: torch.Tensor) -> None:
+        """Synchronous form: the all-reduce on the caller's current stream itself (no event hop to this group's
+        stream and back); the result is ready for whatever the current stream runs next."""
+        cur = torch.cuda.current_stream(self.device).cuda_stream
+        _check(_lib().dllm_nccl_all_reduce(self.comm, t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype], cur),
+               "ncclAllReduce")
+
     def all_gather_into(self, out: torch.Tensor, shard: torch.Tensor) -> NativeWork:
         if out.numel() != shard.numel() * self._size:
             raise ValueError("all_gather_into: size mismatch")

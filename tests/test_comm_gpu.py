@@ -172,3 +172,24 @@ def test_elided_collective_keeps_dependency(pg):
     torch.cuda.synchronize()
     assert torch.all(y == 2.0)
     mesh.destroy()
+
+
+@pytest.mark.parametrize("backend", ["torch", "native"])
+def test_sync_all_reduce_on_current_stream_orders(pg, backend):
+    """A synchronous all-reduce (async_op=False: on the caller's stream, no communicator-stream hop) sits between the
+    compute stream's producer and consumer kernels."""
+    from dllm.parallel import comm
+
+    dev = torch.device("cuda", 0)
+    mesh = Mesh.build(1, 1, force=True, comm_backend=backend, device=dev)
+    x = torch.zeros(1 << 22, device=dev)
+    for _ in range(5):
+        x.add_(1.0)
+        assert isinstance(comm.all_reduce(x, mesh.group("tp"), async_op=False), comm.Done)
+        x.mul_(2.0)
+    torch.cuda.synchronize()
+    want = 0.0
+    for _ in range(5):
+        want = (want + 1.0) * 2.0
+    assert torch.all(x == want)
+    mesh.destroy()
