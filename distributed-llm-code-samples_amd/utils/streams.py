@@ -7,7 +7,14 @@ stream can land on the compute stream's queue and the two streams' kernels seria
 (``profiles/r3/hw_queue_collision_trace_r3.txt``: the weight-gradient stream lost all of its overlap that way).
 
 ``DLLM_SIDE_STREAMS`` picks the remedy:
-  * ``pool`` (default): torch pool streams;
+  * ``role`` (default since round 4): the FSDP side stream (shard updates and the step-boundary update -> gather
+    chains) is a native high-priority stream, every other role a torch pool stream.  On the pool, the FSDP stream
+    shared a hardware queue with ProcessGroupNCCL's collective streams, so a collective's completion marker waited
+    behind a shard update and the compute stream behind the marker: forced-comm hybrid (FSDP x TP) 172.7 / 172.9 vs
+    173.5 / 174.2 ms with its exposed_ms_diff 0.8-1.0 vs 3.8-3.9 ms, FSDP 32.39 / 32.45 vs 32.44 / 32.72 ms, one box
+    (``profiles/r4/side_streams_high_fsdp_r4.txt``).  ZeRO's optimizer stream loses at high priority (32.54-32.60 vs
+    32.25 ms) and stays on the pool;
+  * ``pool``: torch pool streams for every role;
   * ``high``: native non-blocking streams at high priority (``csrc/comm.cpp: dllm_stream_create``).  HIP keeps a
     separate queue set per priority, and nothing else in the process asks for high-priority queues, so these
     never share the compute stream's (normal-priority) queue;
@@ -50,18 +57,20 @@ _HANDLES: dict[tuple[int, str], torch.cuda.ExternalStream] = {}
 
 
 HIGH_ROLES_AUTO = ("wgrad",)
+HIGH_ROLES = ("fsdp",)
 
 
 def mode() -> str:
-    m = os.environ.get("DLLM_SIDE_STREAMS", "pool")
-    if m not in ("pool", "high", "auto"):
-        raise ValueError(f"DLLM_SIDE_STREAMS={m!r}: expected pool | high | auto")
+    m = os.environ.get("DLLM_SIDE_STREAMS", "role")
+    if m not in ("role", "pool", "high", "auto"):
+        raise ValueError(f"DLLM_SIDE_STREAMS={m!r}: expected role | pool | high | auto")
     return m
 
 
 def high_priority(role: str) -> bool:
     m = mode()
-    return m == "high" or (m == "auto" and role in HIGH_ROLES_AUTO)
+    return (m == "high" or (m == "auto" and role in HIGH_ROLES_AUTO)
+            or (m == "role" and role in HIGH_ROLES))
 
 
 def _destroy(handle: int, idx: int) -> None:

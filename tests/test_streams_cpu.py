@@ -7,7 +7,10 @@ from dllm.utils import streams
 
 def test_mode_default_and_validation(monkeypatch):
     monkeypatch.delenv("DLLM_SIDE_STREAMS", raising=False)
-    assert streams.mode() == "pool" and not streams.high_priority("wgrad")
+    assert streams.mode() == "role" and streams.high_priority("fsdp")
+    assert not streams.high_priority("wgrad") and not streams.high_priority("opt")
+    monkeypatch.setenv("DLLM_SIDE_STREAMS", "pool")
+    assert not streams.high_priority("fsdp")
     monkeypatch.setenv("DLLM_SIDE_STREAMS", "auto")
     assert streams.high_priority("wgrad") and not streams.high_priority("opt") and not streams.high_priority("fsdp")
     monkeypatch.setenv("DLLM_SIDE_STREAMS", "high")
