@@ -860,8 +860,9 @@ class FFNTrainer:
             self._fsdp_finish_rs(slot)
             return
         lay, works = pend
-        for w in works.values():
-            w.wait()
+        if not self.fsdp_alias:   # dp = 1: no gradient ring slot to protect, the side stream's own wait suffices
+            for w in works.values():
+                w.wait()
         with torch.cuda.stream(st):
             self._fsdp_finish_rs(slot)
             ev = torch.cuda.Event()

@@ -193,3 +193,28 @@ def test_sync_all_reduce_on_current_stream_orders(pg, backend):
         want = (want + 1.0) * 2.0
     assert torch.all(x == want)
     mesh.destroy()
+
+
+def test_fsdp_side_stream_priority_bitwise(pg, monkeypatch):
+    """The default side-stream policy puts the FSDP stream at high priority (utils/streams.py ``role``): only where
+    the shard updates and step-boundary gathers are queued changes, so the result is bitwise the all-pool run's."""
+    outs = []
+    for mode in ("role", "pool"):
+        monkeypatch.setenv("DLLM_SIDE_STREAMS", mode)
+        D, F, L, T = 256, 1024, 3, 512
+        gen = torch.Generator().manual_seed(21)
+        layers = [init_ffn_layer(D, F, gen) for _ in range(L)]
+        cfg = TrainConfig(model=ModelConfig(D, F, L), batch_size=1, seq_len=T, dtype="bf16", grad_dtype="bf16",
+                          lr=1e-2, dp_mode="fsdp", force_comm=True, comm_backend="torch")
+        dev = torch.device("cuda", 0)
+        mesh = Mesh.build(1, 1, force=True, comm_backend="torch", device=dev)
+        eng = FFNTrainer(cfg, mesh, dev)
+        assert isinstance(eng.fsdp_stream, torch.cuda.ExternalStream) == (mode == "role")
+        eng.load_full_params(layers)
+        for x, dy in reference_mock_data(torch.tensor([5, 6, 7]), T, D):
+            eng.train_step(x.to(dev, torch.bfloat16), dy.to(dev, torch.bfloat16))
+        eng.fsdp_sync()
+        torch.cuda.synchronize()
+        outs.append(eng.master.clone())
+        mesh.destroy()
+    assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
