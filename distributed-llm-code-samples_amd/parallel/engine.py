@@ -860,7 +860,9 @@ class FFNTrainer:
             self._fsdp_finish_rs(slot)
             return
         lay, works = pend
-        if not self.fsdp_alias:   # dp = 1: no gradient ring slot to protect, the side stream's own wait suffices
+        # dp = 1: no gradient ring slot to protect, the side stream's own wait suffices (hybrid 171.7 / 172.2 vs
+        # 172.4 / 172.7 ms with the wait, profiles/r4/fsdp_dp1_rs_wait_r4.txt)
+        if not self.fsdp_alias:
             for w in works.values():
                 w.wait()
         with torch.cuda.stream(st):
