@@ -28,8 +28,6 @@ a GPU tensor with the native library missing raises.
 """
 from __future__ import annotations
 
-import os
-
 import torch
 
 from .. import _native
@@ -226,9 +224,6 @@ def set_splitk(enabled: bool) -> bool:
 
 
 _VARIANT = {"name": "auto"}
-# experiment knob: epilogues (comma list, e.g. "adam_split") whose GEMMs run on the 256x128 two-blocks-per-CU family
-# whatever the global variant -- one block's optimizer epilogue under the other's MFMAs
-_PP_EPIS = frozenset(e for e in os.environ.get("DLLM_PP_EPI", "").split(",") if e)
 # Launch policy of the 256x256 bf16 kernels (tiles per persistent block, minimum blocks per CU): Python-level
 # defaults that every call passes to the library explicitly -- the native side keeps no mutable state, so
 # GEMMs issued concurrently on different streams never race on a setting.
@@ -337,7 +332,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
                      opt_v.data_ptr() if opt_v is not None else None, ksplit,
                      ws.data_ptr() if ws is not None else None,
                      _mask_ptr(mask, M, N) if mask is not None else None,
-                     BF16_VARIANTS["pp" if epi in _PP_EPIS else _VARIANT["name"]], _POLICY["tpb"], _POLICY["min_bpc"])
+                     BF16_VARIANTS[_VARIANT["name"]], _POLICY["tpb"], _POLICY["min_bpc"])
     _native.check(rc, f"dllm_gemm({layout},{epi},M={M},N={N},K={K})")
     if obs is not None:
         obs.gemm_end()
