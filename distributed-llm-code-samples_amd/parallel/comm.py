@@ -154,11 +154,12 @@ def _issue(group, fn, moves: bool = True):
 
 
 def all_reduce(t: torch.Tensor, group, async_op: bool = True):
-    """``async_op=False`` (a consumer right behind it, e.g. the TP forward's output exchange): the collective is
-    enqueued on the caller's current stream -- native: ``NativeGroup.all_reduce_inline``; torch: ProcessGroupNCCL
-    launches synchronous collectives on the current stream -- so it costs no event hops to a communicator stream and
-    back, each a cross-queue wait (``profiles/r4/forced_comm_gaps_r4.txt``).  Under a ``CommObserver`` it stays on
-    the communicator stream, where the observer times it."""
+    """``async_op=False`` (a consumer right behind it, e.g. the TP forward's output exchange): issued as a synchronous
+    collective -- native: ``NativeGroup.all_reduce_inline``, on the caller's current stream, so it costs no event
+    hops to a communicator stream and back, each a cross-queue wait (``profiles/r4/forced_comm_gaps_r4.txt``);
+    torch: ``dist.all_reduce(async_op=False)``, which recent ProcessGroupNCCL versions also launch on the current
+    stream (older ones wait on their own stream, as the async form + wait does).  Under a ``CommObserver`` it stays
+    on the communicator stream, where the observer times it."""
     if _ELIDE and group is not None:
         return Elided(t)
     inline = not async_op and not _SERIALIZE and observe.active() is None and _SYNC_INLINE
