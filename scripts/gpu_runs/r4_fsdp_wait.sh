@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 4: FSDP at dp = 1 without the compute-stream wait on the reduce-scatters (no ring slot to protect) vs with it
+# Round 4 (A/B knob since removed; profiles/r4/fsdp_dp1_rs_wait_r4.txt): FSDP at dp = 1 without the compute-stream wait on the reduce-scatters (no ring slot to protect) vs with it
 # (DLLM_FSDP_ALIAS_WAIT=1), interleaved; the comm tests (race screens, side-stream priority bitwise).
 source scripts/gpu_steps.sh
 step pytest_comm 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_comm_gpu.py
