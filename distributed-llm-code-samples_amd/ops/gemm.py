@@ -28,6 +28,8 @@ a GPU tensor with the native library missing raises.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .. import _native
@@ -224,6 +226,7 @@ def set_splitk(enabled: bool) -> bool:
 
 
 _VARIANT = {"name": "auto"}
+_LIB_NT_STORE = os.environ.get("DLLM_NT_STORE_LIB") == "1"
 # Launch policy of the 256x256 bf16 kernels (tiles per persistent block, minimum blocks per CU): Python-level
 # defaults that every call passes to the library explicitly -- the native side keeps no mutable state, so
 # GEMMs issued concurrently on different streams never race on a setting.
@@ -292,6 +295,11 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
 
     for t, nm in ((a, "a"), (b, "b"), (out, "out")):
         _check_rowmajor(t, nm)
+    if (_LIB_NT_STORE and layout == "nt" and epi == "store" and mask is None and alpha == 1.0 and beta == 0.0
+            and a.dtype == torch.bfloat16 and out.dtype == torch.bfloat16 and K >= 8192 and force is None):
+        # A/B knob (DLLM_NT_STORE_LIB=1): the plain long-K NT store (the forward's second GEMM) through hipBLASLt
+        torch.matmul(a, b.t(), out=out)
+        return out
     if (a.dtype == torch.float32 and mask is None and _use_bf16x6(M, N, K, force)
             and all(t.data_ptr() % 16 == 0 and t.stride(0) % 4 == 0 for t in (a, b))):
         # fp32-accurate GEMM on the bf16 matrix cores: split both operands into three bf16 parts and run one
