@@ -226,7 +226,21 @@ def set_splitk(enabled: bool) -> bool:
 
 
 _VARIANT = {"name": "auto"}
-_LIB_NT_STORE = os.environ.get("DLLM_NT_STORE_LIB") == "1"
+# The plain long-K NT store (the forward's second GEMM, y = a·W2ᵀ with K = F) is the one FFN GEMM where hipBLASLt's
+# kernel beats the native family (1570 vs 1481 TF isolated, profiles/r4/gemm_vs_hipblaslt_r4.txt; flagship step
+# 29.39-29.40 vs 29.46-29.67 ms, profiles/r4/fwd2_hipblaslt_r4.txt).  The engine enables it on single-rank meshes only:
+# under collectives that hold CUs hipBLASLt's non-persistent grids lose 32-40 % (profiles/interference_r1.log) where
+# the persistent native kernels lose nothing.  DLLM_NT_STORE_LIB=0 / 1 forces it off / on.
+_LIB_NT_STORE = {"enabled": False, "env": os.environ.get("DLLM_NT_STORE_LIB")}
+
+
+def set_lib_nt_store(enabled: bool) -> bool:
+    """Route the plain long-K bf16 NT store through hipBLASLt (the environment's DLLM_NT_STORE_LIB wins); returns the
+    previous setting."""
+    old = _LIB_NT_STORE["enabled"]
+    env = _LIB_NT_STORE["env"]
+    _LIB_NT_STORE["enabled"] = (env == "1") if env in ("0", "1") else bool(enabled)
+    return old
 # Launch policy of the 256x256 bf16 kernels (tiles per persistent block, minimum blocks per CU): Python-level
 # defaults that every call passes to the library explicitly -- the native side keeps no mutable state, so
 # GEMMs issued concurrently on different streams never race on a setting.
@@ -295,10 +309,10 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
 
     for t, nm in ((a, "a"), (b, "b"), (out, "out")):
         _check_rowmajor(t, nm)
-    if (_LIB_NT_STORE and layout == "nt" and epi == "store" and mask is None and alpha == 1.0 and beta == 0.0
-            and a.dtype == torch.bfloat16 and out.dtype == torch.bfloat16 and K >= 8192 and force is None):
-        # A/B knob (DLLM_NT_STORE_LIB=1): the plain long-K NT store (the forward's second GEMM) through hipBLASLt
-        torch.matmul(a, b.t(), out=out)
+    if (_LIB_NT_STORE["enabled"] and layout == "nt" and epi == "store" and mask is None and alpha == 1.0
+            and beta == 0.0 and a.dtype == torch.bfloat16 and out.dtype == torch.bfloat16 and K >= 8192
+            and force is None):
+        torch.matmul(a, b.t(), out=out)   # hipBLASLt (see _LIB_NT_STORE)
         return out
     if (a.dtype == torch.float32 and mask is None and _use_bf16x6(M, N, K, force)
             and all(t.data_ptr() % 16 == 0 and t.stride(0) % 4 == 0 for t in (a, b))):

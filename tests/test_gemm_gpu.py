@@ -505,3 +505,26 @@ def test_race_screen_repeated_runs_bitwise(layout, M, N, K, family):
     got = first[:256].cpu().double()
     assert ((got - ref).abs().max() / ref.abs().max()) < 1e-5
 
+
+
+def test_lib_nt_store_routes_only_the_plain_long_k_store():
+    """The forward's plain long-K NT store can go through hipBLASLt (single-rank engines): same product within bf16
+    rounding; epilogue GEMMs, masks, short K and forced paths stay native."""
+    import sys
+
+    G = sys.modules["dllm.ops.gemm"]
+    g = torch.Generator().manual_seed(3)
+    a = torch.randn(512, 8192, generator=g).to(torch.bfloat16).to(DEV)
+    b = torch.randn(768, 8192, generator=g).to(torch.bfloat16).to(DEV)
+    nat = gemm(a, b, "nt")
+    old = G.set_lib_nt_store(True)
+    try:
+        lib = gemm(a, b, "nt")
+        forced = gemm(a, b, "nt", force="mfma_bf16")
+    finally:
+        G._LIB_NT_STORE["enabled"] = old
+    torch.cuda.synchronize()
+    ref = a.double() @ b.double().t()
+    for o in (nat, lib, forced):
+        assert ((o.double() - ref).abs().max() / ref.abs().max()).item() < 1e-2
+    assert torch.equal(forced.view(torch.int16), nat.view(torch.int16))
