@@ -228,19 +228,16 @@ def set_splitk(enabled: bool) -> bool:
 _VARIANT = {"name": "auto"}
 # The plain long-K NT store (the forward's second GEMM, y = a·W2ᵀ with K = F) is the one FFN GEMM where hipBLASLt's
 # kernel beats the native family (1570 vs 1481 TF isolated, profiles/r4/gemm_vs_hipblaslt_r4.txt; flagship step
-# 29.39-29.40 vs 29.46-29.67 ms, profiles/r4/fwd2_hipblaslt_r4.txt).  The engine enables it on single-rank meshes only:
-# under collectives that hold CUs hipBLASLt's non-persistent grids lose 32-40 % (profiles/interference_r1.log) where
-# the persistent native kernels lose nothing.  DLLM_NT_STORE_LIB=0 / 1 forces it off / on.
-_LIB_NT_STORE = {"enabled": False, "env": os.environ.get("DLLM_NT_STORE_LIB")}
+# 29.30-29.40 vs 29.46-29.67 ms, profiles/r4/fwd2_hipblaslt_r4.txt).  A caller opts in per call (``library=True``);
+# the engine does so for that GEMM on single-rank meshes only: under collectives that hold CUs hipBLASLt's
+# non-persistent grids lose 32-40 % (profiles/interference_r1.log) where the persistent native kernels lose nothing.
+# DLLM_NT_STORE_LIB=0 / 1 overrides the engine's choice.
+LIB_NT_STORE_ENV = os.environ.get("DLLM_NT_STORE_LIB")
 
 
-def set_lib_nt_store(enabled: bool) -> bool:
-    """Route the plain long-K bf16 NT store through hipBLASLt (the environment's DLLM_NT_STORE_LIB wins); returns the
-    previous setting."""
-    old = _LIB_NT_STORE["enabled"]
-    env = _LIB_NT_STORE["env"]
-    _LIB_NT_STORE["enabled"] = (env == "1") if env in ("0", "1") else bool(enabled)
-    return old
+def lib_nt_store_default(single_rank: bool) -> bool:
+    """Whether an engine routes its forward's plain long-K NT store to hipBLASLt (``gemm(..., library=True)``)."""
+    return (LIB_NT_STORE_ENV == "1") if LIB_NT_STORE_ENV in ("0", "1") else bool(single_rank)
 # Launch policy of the 256x256 bf16 kernels (tiles per persistent block, minimum blocks per CU): Python-level
 # defaults that every call passes to the library explicitly -- the native side keeps no mutable state, so
 # GEMMs issued concurrently on different streams never race on a setting.
@@ -267,10 +264,12 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
          alpha: float = 1.0, beta: float = 0.0, out_dtype: torch.dtype | None = None, group_m: int | None = None,
          force: str | None = None, lr: float = 0.0, betas: tuple = (0.9, 0.95), eps: float = 1e-8,
          wd: float = 0.0, step: int = 0, opt_m: torch.Tensor | None = None,
-         opt_v: torch.Tensor | None = None, mask: torch.Tensor | None = None) -> torch.Tensor:
+         opt_v: torch.Tensor | None = None, mask: torch.Tensor | None = None,
+         library: bool = False) -> torch.Tensor:
     """``mask`` (ReLU only, GPU, see ``relu_mask_supported``): ``epi="act"`` also writes the activation-gradient
     bitmask, ``epi="dact"`` reads it instead of ``aux`` (1 bit instead of a bf16 per element).  CPU tensors
-    ignore it (``aux`` stays the source of truth there)."""
+    ignore it (``aux`` stays the source of truth there).  ``library``: a plain bf16 NT store with K >= 8192 runs
+    through hipBLASLt (see ``lib_nt_store_default``); any other GEMM ignores it."""
     M, N, K = gemm_shape(a, b, layout)
     if group_m is None:   # raster band height: the layout's policy (profiles/r3/group_m_sweep_r3.txt)
         group_m = _POLICY["group_m_nt"] if layout == "nt" else 4
@@ -309,10 +308,9 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
 
     for t, nm in ((a, "a"), (b, "b"), (out, "out")):
         _check_rowmajor(t, nm)
-    if (_LIB_NT_STORE["enabled"] and layout == "nt" and epi == "store" and mask is None and alpha == 1.0
-            and beta == 0.0 and a.dtype == torch.bfloat16 and out.dtype == torch.bfloat16 and K >= 8192
-            and force is None):
-        torch.matmul(a, b.t(), out=out)   # hipBLASLt (see _LIB_NT_STORE)
+    if (library and layout == "nt" and epi == "store" and mask is None and alpha == 1.0 and beta == 0.0
+            and a.dtype == torch.bfloat16 and out.dtype == torch.bfloat16 and K >= 8192 and force is None):
+        torch.matmul(a, b.t(), out=out)   # hipBLASLt (see lib_nt_store_default)
         return out
     if (a.dtype == torch.float32 and mask is None and _use_bf16x6(M, N, K, force)
             and all(t.data_ptr() % 16 == 0 and t.stride(0) % 4 == 0 for t in (a, b))):

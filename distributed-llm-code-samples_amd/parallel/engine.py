@@ -157,8 +157,12 @@ class FFNTrainer:
                       and use_m224(self.F_loc, T) and use_m224(self.F_loc, D) and T % 256 == 0)
         self.step_count = 0
         dev = self.device
+        # the forward's plain long-K NT store through hipBLASLt, where no collective holds CUs (ops/gemm.py)
+        from ..ops.gemm import lib_nt_store_default
+
+        self.lib_fwd2 = dev.type == "cuda" and lib_nt_store_default(mesh.world == 1)
         if dev.type == "cuda":
-            from ..ops.gemm import set_fp32_mode, set_lib_nt_store, set_min_blocks_per_cu, set_tiles_per_block
+            from ..ops.gemm import set_fp32_mode, set_min_blocks_per_cu, set_tiles_per_block
 
             # gated stacks too since round 3 (persistent GLU / DGLU epilogues): L32 SwiGLU 167.6 vs 168.8 ms
             # (profiles/r3/gated_llama_dims_tpb_wgs_r3.txt)
@@ -169,8 +173,7 @@ class FFNTrainer:
             # with one: hybrid 172.2-172.4 vs 175.8-176.1 ms, zero 30.5-30.7 vs 30.9-31.0
             # (profiles/r4/min_bpc_forcecomm_r4.txt)
             set_min_blocks_per_cu(cfg.gemm_min_bpc or (2 if mesh.world > 1 else 1))
-            # the forward's plain long-K NT store through hipBLASLt, where no collective holds CUs (ops/gemm.py)
-            set_lib_nt_store(mesh.world == 1)
+
         if cfg.debug_sync:
             comm.set_serialize(True)
         # custom xGMI all-reduce for the TP activation exchange (opt-in; gradients stay on RCCL)
@@ -1019,7 +1022,7 @@ class FFNTrainer:
                     layer_fwd_t(self.xs[l], w1, w2, act, a, h, self.xs[l + 1], before_fwd2=before2, mask=self._mask(l))
                 else:
                     layer_fwd(self.xs[l], w1, w2, act, gated, a, h, self.xs[l + 1], before_fwd2=before2,
-                              mask=self._mask(l))
+                              mask=self._mask(l), library_fwd2=self.lib_fwd2)
                 if self.tp_comm:
                     last = l == L - 1
                     if self.tp_car is not None:

@@ -48,14 +48,3 @@ def free_port():
         if all(_bindable(_PORT[0] + k) for k in range(10)):
             return _PORT[0]
 
-
-@pytest.fixture(autouse=True)
-def _native_nt_store():
-    """Kernel tests exercise the native GEMMs: an engine built by an earlier test may have routed the plain long-K NT
-    store to hipBLASLt (ops/gemm.py ``set_lib_nt_store``); start every test with it off."""
-    import sys as _sys
-
-    g = _sys.modules.get("dllm.ops.gemm")
-    if g is not None:
-        g._LIB_NT_STORE["enabled"] = False
-    yield

@@ -508,21 +508,14 @@ def test_race_screen_repeated_runs_bitwise(layout, M, N, K, family):
 
 
 def test_lib_nt_store_routes_only_the_plain_long_k_store():
-    """The forward's plain long-K NT store can go through hipBLASLt (single-rank engines): same product within bf16
-    rounding; epilogue GEMMs, masks, short K and forced paths stay native."""
-    import sys
-
-    G = sys.modules["dllm.ops.gemm"]
+    """``library=True`` sends the plain long-K NT store through hipBLASLt (the engine's forward on single-rank
+    meshes): same product within bf16 rounding; forced paths stay native."""
     g = torch.Generator().manual_seed(3)
     a = torch.randn(512, 8192, generator=g).to(torch.bfloat16).to(DEV)
     b = torch.randn(768, 8192, generator=g).to(torch.bfloat16).to(DEV)
     nat = gemm(a, b, "nt")
-    old = G.set_lib_nt_store(True)
-    try:
-        lib = gemm(a, b, "nt")
-        forced = gemm(a, b, "nt", force="mfma_bf16")
-    finally:
-        G._LIB_NT_STORE["enabled"] = old
+    lib = gemm(a, b, "nt", library=True)
+    forced = gemm(a, b, "nt", library=True, force="mfma_bf16")
     torch.cuda.synchronize()
     ref = a.double() @ b.double().t()
     for o in (nat, lib, forced):
