@@ -128,7 +128,14 @@ def parse(argv=None):
     p.add_argument("--methods", default="ddp,zero,fsdp,tp,hybrid",
                    help="comma list of methods also timed side by side ('' or 'none' = headline only)")
     p.add_argument("--method_steps", type=int, default=0,
-                   help="timed steps per side-by-side method (0 = min(steps, 10))")
+                   help="minimum timed steps per side-by-side method (0 = min(steps, 10)); see --side_timed_ms")
+    p.add_argument("--side_warmup_ms", type=float, default=150.0,
+                   help="side-by-side methods: after min(warmup, 3) steps keep warming up until this much step time "
+                        "has run (the GPU clock ramps over its first ~50 ms of load, profiles/r4/window_probe_r4.txt)")
+    p.add_argument("--side_timed_ms", type=float, default=300.0,
+                   help="side-by-side methods: time at least max(method steps, ceil(this / step time)) steps")
+    p.add_argument("--side_max_steps", type=int, default=1000,
+                   help="cap on the timed steps of one side-by-side method")
     p.add_argument("--side_deadline_s", type=float, default=420.0,
                    help="wall-clock budget of the side-by-side methods after the headline (0 = none): past it, rank 0 "
                         "prints the line with the methods finished so far and every rank exits")
@@ -173,8 +180,10 @@ def parse(argv=None):
                         "update into the wgrad GEMM epilogue)")
     p.add_argument("--phases", action="store_true",
                    help="also report per-phase GPU time (forward / backward / optimizer tail) from HIP events")
-    p.add_argument("--tp_allreduce", choices=["rccl", "custom"], default="rccl",
-                   help="TP activation all-reduce: RCCL, or the custom two-shot xGMI peer all-reduce (csrc/car.hip)")
+    p.add_argument("--tp_allreduce", choices=["rccl", "custom", "auto"], default="rccl",
+                   help="TP activation all-reduce: RCCL, the custom two-shot xGMI peer all-reduce (csrc/car.hip), or auto "
+                        "(both timed on the [T, D] message at engine build on the real tp group, the faster kept; "
+                        "the timings go to the method's tp_allreduce_choice)")
     p.add_argument("--gemm_variant", default="auto",
                    choices=["auto", "2stage", "8phase", "8phase_stagger", "4phase_stagger", "pp"],
                    help="bf16 GEMM main-loop schedule (auto = 8-phase staggered when K %% 128 == 0; pp = 256x128 tiles, "
@@ -281,9 +290,14 @@ def destroy_mesh(mesh: Mesh) -> None:
 
 
 def run_method(a, method: str, n: int, world: int, dev: torch.device, steps: int, warmup: int,
-               force_comm: bool, model: ModelConfig, observe_steps: int = 0, headline: bool = False) -> dict:
+               force_comm: bool, model: ModelConfig, observe_steps: int = 0, headline: bool = False,
+               windows: tuple = (0.0, 0.0, 0), fsdp_alias: bool = True) -> dict:
     """Build the engine for ``method`` on ``n`` ranks, run ``warmup`` untimed + ``steps`` timed steps (+ the
-    observed steps), return the method's record.  Collective over all ranks."""
+    observed steps), return the method's record.  Collective over all ranks.
+
+    ``windows`` = (min warm-up ms, min timed ms, max timed steps): the side-by-side methods' steady-state windows
+    (the headline keeps the driver's exact step counts: (0, 0, 0)).  ``fsdp_alias`` False: FSDP at dp = 1 runs its
+    gather / gradient rings and real (copying) size-1 collectives instead of aliasing the full buffers."""
     cpu = dev.type == "cpu"
     dp_mode, dp, tp = mesh_of(method, n, a.tp)
     cfg = TrainConfig(model=model, batch_size=a.batch_size, seq_len=a.seq_len, num_steps=steps, dtype=a.dtype,
@@ -295,12 +309,12 @@ def run_method(a, method: str, n: int, world: int, dev: torch.device, steps: int
                       relu_mask=not a.no_relu_mask, gemm_tiles_per_block=a.tpb, fp32_gemm=a.fp32_gemm,
                       gemm_min_bpc=a.min_bpc, master=a.master, wgrad_stream_max_tpc=a.wgrad_stream_max_tpc,
                       wgrad_stream=a.wgrad_stream and headline and not a.graph,
-                      tp_transposed=os.environ.get("DLLM_TP_TRANSPOSED", "1") != "0")
+                      tp_transposed=os.environ.get("DLLM_TP_TRANSPOSED", "1") != "0", fsdp_alias=fsdp_alias)
     mesh = Mesh.build(dp, tp, force=force_comm, comm_backend="torch" if cpu else a.comm,
                       device=None if cpu else dev)
     try:
         return _run_on_mesh(a, method, cfg, mesh, n, world, dev, steps, warmup, force_comm, model, observe_steps,
-                            headline)
+                            headline, windows)
     except BaseException:
         # error path (e.g. out of memory on one rank): abort this method's communicators, so they neither leak
         # into the next method nor block in a synchronising teardown against peers that moved on
@@ -308,7 +322,19 @@ def run_method(a, method: str, n: int, world: int, dev: torch.device, steps: int
         raise
 
 
-def _run_on_mesh(a, method, cfg, mesh, n, world, dev, steps, warmup, force_comm, model, observe_steps, headline):
+def _agree_max(x: float, world: int, dev) -> float:
+    """The maximum of ``x`` over all ranks (every rank must take the same number of steps)."""
+    if world <= 1:
+        return x
+    import torch.distributed as dist
+
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def _run_on_mesh(a, method, cfg, mesh, n, world, dev, steps, warmup, force_comm, model, observe_steps, headline,
+                 windows=(0.0, 0.0, 0)):
     cpu = dev.type == "cpu"
     sync = (lambda: None) if cpu else torch.cuda.synchronize
     dp, tp = cfg.dp, cfg.tp
@@ -346,24 +372,57 @@ def _run_on_mesh(a, method, cfg, mesh, n, world, dev, steps, warmup, force_comm,
             if old is not None:
                 comm.set_elide(old)
 
+    min_warm_ms, min_timed_ms, max_steps = windows
+    t_w = time.perf_counter()
     for i in range(warmup):
         one_step(seed_base + i)
+    nwarm = warmup
+    if min_warm_ms > 0 or min_timed_ms > 0:
+        # steady-state windows (side methods): warm up on GPU time, not a step count -- the clock ramps over the first
+        # ~50 ms of load -- in doubling batches of timed steps (first steps are slow: allocation, queue creation) until
+        # the warm-up reaches min_warm_ms; the last batch's step time sizes the timed window (+20 % margin); every
+        # rank agrees on every count
+        sync()
+        batch, step_ms = 1, float("inf")
+        while True:
+            t1 = time.perf_counter()
+            for i in range(batch):
+                one_step(seed_base + nwarm + i)
+            sync()
+            dt = _agree_max((time.perf_counter() - t1) * 1e3, world, dev)
+            nwarm += batch
+            if batch >= 2:   # the fastest multi-step batch: the first steps (allocation, queue creation) read slow
+                step_ms = min(step_ms, dt / batch)
+            if _agree_max((time.perf_counter() - t_w) * 1e3, world, dev) >= min_warm_ms and batch >= 2:
+                break
+            batch *= 2
+        steps = max(steps, min(max_steps or steps, int(-(-1.2 * min_timed_ms // max(step_ms, 1e-3)))))
+    warm_total_ms = _agree_max((time.perf_counter() - t_w) * 1e3, world, dev) if (min_warm_ms > 0 or min_timed_ms > 0) \
+        else (time.perf_counter() - t_w) * 1e3
     queues = None
     if not cpu and a.backend == "nccl":
         # every stream of this method exists and has run by now: measure which share the compute stream's queue
         from dllm.utils.streams import queue_report
 
         sync()
-        queues = queue_report(dev, {"wgrad": eng.wg_stream, "opt": getattr(eng, "opt_stream", None),
-                                    "fsdp": getattr(eng, "fsdp_stream", None),
-                                    "data": getattr(data, "_stream", None)})
+        sides = {"wgrad": eng.wg_stream, "opt": getattr(eng, "opt_stream", None),
+                 "fsdp": getattr(eng, "fsdp_stream", None), "data": getattr(data, "_stream", None)}
+        queues = queue_report(dev, sides)
+        if mesh.groups:
+            # pairwise: role communicators' streams (identified at mesh build) and the side streams; conflicts =
+            # any of them on the compute queue, or the FSDP gather and reduce-scatter on one queue
+            from dllm.utils.streams import role_queue_report
+
+            named = {r: mesh.role_streams.get(r) for r in mesh.groups if mesh.groups[r] is not None}
+            named.update({k: v for k, v in sides.items() if v is not None})
+            queues.update(role_queue_report(dev, named))
     if a.phases and headline and not cpu and graphed is None:
         eng.enable_phase_timing(True)
     sync()
     comm.barrier(device=dev)
     t0 = time.perf_counter()
     for i in range(steps):
-        one_step(seed_base + warmup + i)
+        one_step(seed_base + nwarm + i)
     sync()
     comm.barrier(device=dev)
     el = time.perf_counter() - t0
@@ -382,12 +441,15 @@ def _run_on_mesh(a, method, cfg, mesh, n, world, dev, steps, warmup, force_comm,
            "finite": bool(torch.isfinite(eng.master_slice(0, 1024)).all().item()),
            "master": "fp32 (split: bf16 working copy + int16 residual)" if eng.split else "fp32",
            "global_batch": a.batch_size * dp, "parallelism": parallelism(method, n, dp, tp, world, force_comm),
-           "model": model_name(model), "steps": steps, "warmup": warmup, "state_gib": state_gib(eng),
+           "model": model_name(model), "steps": steps, "warmup": nwarm, "state_gib": state_gib(eng),
+           "warmup_ms": round(warm_total_ms, 1), "timed_ms": round(el * 1e3, 1),
            "wgrad_stream": eng.wg_stream is not None,
            # small-grid weight gradients in one grouped launch / F-major activations on 224-row tiles (MP at tp 8)
            "pair_wgrads": bool(eng.pair_wgrads), "tp_transposed": bool(eng.tmode),
            # the ranks each role communicator actually spans (RCCL / gloo group sizes; {} = no collective)
            "comm_sizes": {role: g.size() for role, g in mesh.groups.items() if g is not None}}
+    if eng.tp_ar_choice is not None:
+        rec["tp_allreduce_choice"] = eng.tp_ar_choice
     if a.elide_collectives:
         rec["collectives_elided"] = True   # diagnostic run: not the method's step time
     if phases:
@@ -395,7 +457,7 @@ def _run_on_mesh(a, method, cfg, mesh, n, world, dev, steps, warmup, force_comm,
     if queues is not None:
         rec["queues"] = queues
     communicates = bool(mesh.groups) or eng.tp_car is not None
-    nxt = seed_base + warmup + steps
+    nxt = seed_base + nwarm + steps
     if observe_steps > 0 and communicates and not cpu and graphed is None:
         from dllm.utils.observe import CommObserver
 
@@ -404,10 +466,18 @@ def _run_on_mesh(a, method, cfg, mesh, n, world, dev, steps, warmup, force_comm,
                 one_step(nxt + i)
         nxt += observe_steps
         rec["comm"] = obs.summary(observe_steps)
+    if "comm" in rec and world == 1:
+        # every collective a size-1 communicator that moved no data (aliased in place): the method's comm numbers say
+        # nothing about collectives at N > 1
+        c = rec["comm"]
+        c["collectives_noop"] = bool(c.get("collectives_per_step")) and \
+            c.get("noop_collectives_per_step") == c.get("collectives_per_step")
     if a.diff_pairs > 0 and a.diff_steps > 0 and communicates and graphed is None and not a.elide_collectives:
         # differential exposed communication: the same engine with its collectives elided (compute only), interleaved
         # with normal steps in this process; the difference of the medians is the step time the collectives add
         on, off = [], []
+        # each segment >= ~100 ms of steps (sub-ms methods: short windows read the clock ramp, not the collectives)
+        dsteps = max(a.diff_steps, min(max_steps or a.diff_steps, int(-(-100.0 // max(el * 1e3 / steps, 1e-3)))))
         for _ in range(a.diff_pairs):
             for elide, acc in ((False, on), (True, off)):
                 old = comm.set_elide(elide)
@@ -415,25 +485,26 @@ def _run_on_mesh(a, method, cfg, mesh, n, world, dev, steps, warmup, force_comm,
                     sync()
                     comm.barrier(device=dev)
                     t1 = time.perf_counter()
-                    for i in range(a.diff_steps):
+                    for i in range(dsteps):
                         one_step(nxt + i)
                     sync()
                     comm.barrier(device=dev)
                     dt = time.perf_counter() - t1
                 finally:
                     comm.set_elide(old)
-                nxt += a.diff_steps
+                nxt += dsteps
                 if world > 1:
                     import torch.distributed as dist
 
                     t = torch.tensor([dt], dtype=torch.float64, device=dev)
                     dist.all_reduce(t, op=dist.ReduceOp.MAX)
                     dt = float(t.item())
-                acc.append(dt / a.diff_steps * 1e3)
+                acc.append(dt / dsteps * 1e3)
         med = lambda v: sorted(v)[len(v) // 2]  # noqa: E731
         c = rec.setdefault("comm", {})
         c["exposed_ms_diff"] = round(med(on) - med(off), 3)
         c["diff_step_ms"] = {"normal": [round(v, 3) for v in on], "collectives_elided": [round(v, 3) for v in off]}
+        c["diff_steps"] = dsteps
     if eng.zero:
         eng.zero_sync_state()  # quiesce in-flight weight all-gathers before teardown
     sync()
@@ -446,7 +517,8 @@ def _run_on_mesh(a, method, cfg, mesh, n, world, dev, steps, warmup, force_comm,
 
 
 SIDE_KEYS = ("value", "ms_per_step", "tflops_per_gpu", "peak_hbm_gib", "parallelism", "model", "global_batch",
-             "steps", "finite", "state_gib", "comm", "queues", "comm_sizes", "pair_wgrads", "tp_transposed")
+             "steps", "warmup", "warmup_ms", "timed_ms", "finite", "state_gib", "comm", "queues", "comm_sizes",
+             "pair_wgrads", "tp_transposed", "tp_allreduce_choice")
 
 
 def main(argv=None) -> int:
@@ -533,8 +605,11 @@ def main(argv=None) -> int:
             rec["methods"] = dict(side)
             if world == 1:
                 rec["methods_note"] = ("N=1: ddp/zero/fsdp/tp/hybrid run their collective code paths over size-1 "
-                                       "communicators; tp is the MP config (hidden 4096, FFN 14336, 1 layer); "
-                                       "hybrid is the Llama-3-8B-dims SwiGLU stack (32 layers) on FSDP x TP")
+                                       "communicators, which alias in place and move no data (comm.collectives_noop); "
+                                       "fsdp_copy is FSDP with real copying size-1 gathers / reduce-scatters; tp is the "
+                                       "MP config (hidden 4096, FFN 14336, 1 layer); hybrid is the Llama-3-8B-dims "
+                                       "SwiGLU stack (32 layers) on FSDP x TP; side methods are timed on steady-state "
+                                       "windows (warmup_ms, timed_ms)")
         if a.force_comm:
             rec["note"] = "force_comm: headline collectives over size-1 RCCL communicators"
         if cpu:
@@ -580,6 +655,10 @@ def main(argv=None) -> int:
         watchdog = threading.Timer(a.side_deadline_s, on_deadline)
         watchdog.daemon = True
         watchdog.start()
+    if world == 1 and "fsdp" in methods and "fsdp_copy" not in methods:
+        # N=1: FSDP's size-1 collectives alias the full buffers and move nothing; fsdp_copy runs the dp > 1 ring
+        # schedule with real (copying) RCCL gathers / reduce-scatters, so its exposed_ms_diff measures collectives
+        methods.insert(methods.index("fsdp") + 1, "fsdp_copy")
     for m in methods:
         current["m"] = m
         mm = model
@@ -590,8 +669,10 @@ def main(argv=None) -> int:
             mm = ModelConfig(model_size=a.model_size, ffn_dim=a.llama_ffn_dim, layers=a.llama_layers, act="silu",
                              gated=True)
         try:
-            r = run_method(a, m, n, world, dev, a.method_steps or min(a.steps, 10), min(a.warmup, 3),
-                           force_comm=(world == 1), model=mm, observe_steps=a.observe_steps)
+            r = run_method(a, "fsdp" if m == "fsdp_copy" else m, n, world, dev, a.method_steps or min(a.steps, 10),
+                           min(a.warmup, 3), force_comm=(world == 1), model=mm, observe_steps=a.observe_steps,
+                           windows=(a.side_warmup_ms, a.side_timed_ms, a.side_max_steps),
+                           fsdp_alias=m != "fsdp_copy")
         except (ValueError, RuntimeError) as e:
             # a side measurement must not cost the headline line (a config / memory error raises on every
             # rank alike; a hang is cut off by the deadline above)

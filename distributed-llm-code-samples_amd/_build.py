@@ -131,7 +131,9 @@ def build(verbose: bool = False, force: bool = False, jobs: int = 0, variant: st
     if not force and os.path.exists(lib_path) and os.path.getmtime(lib_path) >= newest:
         return lib_path
     tdir = _torch_lib_dir()
-    link = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", lib_path + ".tmp"]
+    # -Bsymbolic: the library's own calls bind inside it, so an A/B build loaded next to the production library
+    # (scripts/bench_gemm.py --libs) runs its own kernels, not the first-loaded library's same-named entry points
+    link = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-Wl,-Bsymbolic", *objs, "-o", lib_path + ".tmp"]
     if tdir and os.path.exists(os.path.join(tdir, "librccl.so")):
         # bind RCCL to torch's bundled copy (same SONAME librccl.so.1 as /opt/rocm's)
         link += [f"-L{tdir}", "-l:librccl.so", f"-Wl,-rpath,{tdir}"]

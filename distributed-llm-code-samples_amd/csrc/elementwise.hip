@@ -418,6 +418,18 @@ int dllm_adam_split_step(void* lo, void* hi, const void* grad, int grad_dtype, f
   return (int)hipGetLastError();
 }
 
+// the same update as dllm_adam_split_step, bitwise, on at most max_blocks workgroups (side-stream AdamW next to GEMMs)
+int dllm_adam_split_step_blocks(void* lo, void* hi, const void* grad, int grad_dtype, float* m, float* v, long n,
+                                float lr, float b1, float b2, float eps, float wd, int step, float gscale, int max_blocks,
+                                void* stream) {
+  if (n % 4 || step < 1 || max_blocks <= 0 || ((uintptr_t)lo | (uintptr_t)hi) % 8) return -1;
+  const float bc1 = 1.f - powf(b1, (float)step), bc2 = 1.f - powf(b2, (float)step);
+  const int g = std::min(grid_for(n / 4), max_blocks);
+  hipLaunchKernelGGL(adam_split_kernel, dim3(g), dim3(256), 0, (hipStream_t)stream, (uint16_t*)lo, (uint16_t*)hi, grad,
+                     grad_dtype, m, v, n, lr, b1, b2, eps, wd, bc1, bc2, gscale);
+  return (int)hipGetLastError();
+}
+
 // mode 0: out_f32 = join(hi, lo);  mode 1: (hi, lo) = split(in_f32)
 int dllm_split_master(void* hi, void* lo, void* f32, long n, int mode, void* stream) {
   if (n <= 0) return 0;
@@ -495,26 +507,35 @@ int dllm_queue_reserve(void* base, int candidates, int spin_us) {
   static int nblock = 0;
   if (candidates <= 0 || candidates > 512) return -1;
   hipStream_t cand[512];
-  int made = 0;
-  for (int i = 0; i < candidates; ++i) {
+  int made = 0, err = 0;
+  for (int i = 0; i < candidates && !err; ++i) {
     if (hipStreamCreateWithFlags(&cand[i], hipStreamNonBlocking) != hipSuccess) break;
     made = i + 1;
     // first use of a stream acquires its queue: do that before the timed probe, so a slow queue creation is not
     // mistaken for sharing
     hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(64), 0, cand[i], (unsigned long long*)nullptr, -1L);
-    if (hipStreamSynchronize(cand[i]) != hipSuccess) return -6;
-    const int sh = dllm_queue_shared(base, (void*)cand[i], spin_us);
-    if (sh < 0) return sh;
-    if (sh == 1 && nblock < 512) {
+    if (hipStreamSynchronize(cand[i]) != hipSuccess) {
+      err = -6;
+      break;
+    }
+    // majority of 3 probes (one can read "shared" when the candidate's dispatch is merely late; a wrongly kept
+    // blocker would raise a non-compute queue's use count and steer later streams onto the compute queue)
+    int votes = 0;
+    for (int t = 0; t < 3 && !err; ++t) {
+      const int sh = dllm_queue_shared(base, (void*)cand[i], spin_us);
+      if (sh < 0) err = sh;
+      else votes += sh;
+    }
+    if (!err && votes >= 2 && nblock < 512) {
       blockers[nblock++] = cand[i];
       cand[i] = nullptr;
     }
   }
-  for (int i = 0; i < made; ++i)
+  for (int i = 0; i < made; ++i)  // every non-blocker candidate, on success and on error alike
     if (cand[i]) (void)hipStreamDestroy(cand[i]);
-  return nblock;
+  return err ? err : nblock;
 }
 
-int dllm_abi_version() { return 11; }
+int dllm_abi_version() { return 12; }
 
 }  // extern "C"

@@ -39,6 +39,9 @@
 #define DLLM_ADAM_PIPE 1  // fused-AdamW epilogue: row groups per batch, the next batch's master / moment loads issued
                           // before this batch's stores (0 = sequential batches; profiles/r2/epilogue_pipe_experiment_r2.log)
 #endif
+#ifndef DLLM_BPRE
+#define DLLM_BPRE 1  // 8-phase kernel: each K-tile's B-half 0 read one phase early (balanced read segments)
+#endif
 #ifndef DLLM_F32_256
 #define DLLM_F32_256 1
 #endif
@@ -1306,6 +1309,12 @@ __device__ __forceinline__ void gemm_8ph_body(const GemmArgs& p, const int which
   Bpf += 2 * b_kstep;
   asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   DLLM_BARRIER();
+#if DLLM_BPRE
+  // B-half 0 of K-tile 0 ahead of the loop (the loop reads every K-tile's B0 one phase before its q0, see below)
+  read_b(I0{}, I0{}, fb0);
+  DLLM_LDS_WAIT();
+  fin_b(fb0);
+#endif
   if constexpr (STAGGER) {
     if (wr == 1) DLLM_BARRIER();
   }
@@ -1316,6 +1325,80 @@ __device__ __forceinline__ void gemm_8ph_body(const GemmArgs& p, const int which
   if (VMWAIT) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");       \
   DLLM_LDS_WAIT();                                                   \
   DLLM_BARRIER();
+#if DLLM_BPRE
+    // Balanced fragment reads (round 5).  The fragment-read segment of phase P overlaps the SIMD partner's MFMA
+    // segment; the old order read A0 + B0 (12 of the K-tile's 24 fragments) before q0 and nothing before q3, so the
+    // q0 segment outlasted the partner's 16 MFMAs.  Here each K-tile's B-half 0 is read one phase early, in the
+    // previous quadrant q3 (into whichever B register set q2 has finished with: fb0 / fb1 alternate per K-tile), so
+    // the segments carry 8 / 4 / 8 / 4 fragments.  The MFMA sequence is unchanged (bitwise the same results).
+    // That read needs the next buffer's B0 retired one phase earlier: vmcnt(8) at P2 / P6 (after the stage, 4
+    // half-tiles left in flight) retires the B0 staged at P6 / P2 before, read at P3 / P7.
+#define DLLM_PHASE_END8()                                           \
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");                   \
+  DLLM_LDS_WAIT();                                                   \
+  DLLM_BARRIER();
+    // ---- even buffer (K-tile 2it); its B0 is in fb0 ----
+    read_a(I0{}, I0{});
+    stage_at(0, 1, Apf - a_kstep, 1);          // P0: A1 odd (K-tile 2it+1)
+    if (it == nk / 2 - 1) {
+      if (next_slot < total) {
+        const GemmArgs q = reload_args(which);
+        Apf = a_base(q, next_slot);
+        Bpf = b_base(q, next_slot);
+      } else {
+        Apf -= 2 * a_kstep;
+        Bpf -= 2 * b_kstep;
+      }
+    }
+    DLLM_PHASE_END(false)
+    fin_a();
+    mfma_quad(acc[0][0], fb0, I0{});
+    DLLM_BARRIER();
+    read_b(I1{}, I0{}, fb1);
+    stage_at(0, 0, Apf, 0);                    // P1: A0 even (K-tile 2it+2)
+    DLLM_PHASE_END(false)
+    fin_b(fb1);
+    mfma_quad(acc[0][1], fb1, I0{});
+    DLLM_BARRIER();
+    read_a(I1{}, I0{});
+    stage_at(1, 0, Bpf, 0);                    // P2: B0 even
+    DLLM_PHASE_END8()
+    fin_a();
+    mfma_quad(acc[1][1], fb1, I1{});
+    DLLM_BARRIER();
+    read_b(I0{}, I1{}, fb1);                   // odd buffer's B0 (retired at P2) -> fb1 (free after q2)
+    stage_at(1, 1, Bpf, 0);                    // P3: B1 even
+    DLLM_PHASE_END(true)
+    fin_b(fb1);
+    mfma_quad(acc[1][0], fb0, I1{});
+    DLLM_BARRIER();
+    // ---- odd buffer (K-tile 2it+1); its B0 is in fb1 ----
+    read_a(I0{}, I1{});
+    stage_at(0, 1, Apf, 0);                    // P4: A1 even
+    DLLM_PHASE_END(false)
+    fin_a();
+    mfma_quad(acc[0][0], fb1, I0{});
+    DLLM_BARRIER();
+    read_b(I1{}, I1{}, fb0);
+    stage_at(0, 0, Apf + a_kstep, 1);          // P5: A0 odd (K-tile 2it+3)
+    DLLM_PHASE_END(false)
+    fin_b(fb0);
+    mfma_quad(acc[0][1], fb0, I0{});
+    DLLM_BARRIER();
+    read_a(I1{}, I1{});
+    stage_at(1, 0, Bpf + b_kstep, 1);          // P6: B0 odd
+    DLLM_PHASE_END8()
+    fin_a();
+    mfma_quad(acc[1][1], fb0, I1{});
+    DLLM_BARRIER();
+    read_b(I0{}, I0{}, fb0);                   // next even B0 (K-tile 2it+2, or the next slot's K-tile 0) -> fb0
+    stage_at(1, 1, Bpf + b_kstep, 1);          // P7: B1 odd
+    DLLM_PHASE_END(true)
+    fin_b(fb0);
+    mfma_quad(acc[1][0], fb1, I1{});
+    DLLM_BARRIER();
+#undef DLLM_PHASE_END8
+#else
     // ---- even buffer (K-tile 2it) ----
     read_a(I0{}, I0{}); read_b(I0{}, I0{}, fb0);
     stage_at(0, 1, Apf - a_kstep, 1);          // P0: A1 odd (K-tile 2it+1)
@@ -1373,6 +1456,7 @@ __device__ __forceinline__ void gemm_8ph_body(const GemmArgs& p, const int which
     DLLM_PHASE_END(true)
     mfma_quad(acc[1][0], fb0, I1{});
     DLLM_BARRIER();
+#endif
     Apf += 2 * a_kstep;
     Bpf += 2 * b_kstep;
 #undef DLLM_PHASE_END

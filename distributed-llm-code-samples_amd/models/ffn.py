@@ -94,18 +94,17 @@ def needs_preact(act: str, gated: bool) -> bool:
 
 def layer_fwd(x: torch.Tensor, w1: torch.Tensor, w2: torch.Tensor, act: str, gated: bool,
               a_out: torch.Tensor, h_out: torch.Tensor | None, y_out: torch.Tensor,
-              before_fwd2=None, mask: torch.Tensor | None = None, library_fwd2: bool = False) -> torch.Tensor:
+              before_fwd2=None, mask: torch.Tensor | None = None) -> torch.Tensor:
     """y = act(x·W1ᵀ)·W2ᵀ  (gated: (act(x·W1ᵀ)⊙x·W3ᵀ)·W2ᵀ with ``w1`` = interleaved W13).
     ``before_fwd2()`` runs between the two GEMMs (e.g. waiting for W2's all-gather).  ``mask`` (ReLU):
-    the first GEMM also writes the activation-gradient bitmask the backward's dgrad reads.  ``library_fwd2``: the
-    second GEMM (a plain store) may run through hipBLASLt (ops/gemm.py ``lib_nt_store_default``)."""
+    the first GEMM also writes the activation-gradient bitmask the backward's dgrad reads."""
     if gated:
         gemm(x, w1, "nt", out=a_out, epi="glu", act=act, aux_out=h_out)
     else:
         gemm(x, w1, "nt", out=a_out, epi="act", act=act, aux_out=h_out, mask=mask)
     if before_fwd2 is not None:
         before_fwd2()
-    gemm(a_out, w2, "nt", out=y_out, library=library_fwd2)
+    gemm(a_out, w2, "nt", out=y_out)
     return y_out
 
 

@@ -28,8 +28,6 @@ a GPU tensor with the native library missing raises.
 """
 from __future__ import annotations
 
-import os
-
 import torch
 
 from .. import _native
@@ -186,7 +184,21 @@ def split3(x: torch.Tensor, role: int, rows_form: bool) -> torch.Tensor:
     return out
 
 
-NUM_CUS = 256
+NUM_CUS = 256   # MI355X; the device's own count is used when a GPU is present (num_cus)
+_NCU: list = []
+
+
+def num_cus() -> int:
+    """Compute units of the current GPU (the native side's tile-grid decisions use the same count, csrc/gemm.hip
+    use_m224 -> num_cu()); 256 (MI355X) without a GPU, e.g. in CPU tests."""
+    if not _NCU:
+        n = NUM_CUS
+        if torch.cuda.is_available():
+            n = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+        _NCU.append(int(n))
+    return _NCU[0]
+
+
 _SPLITK = {"enabled": True}
 
 
@@ -200,7 +212,7 @@ def choose_ksplit(M: int, N: int, K: int) -> int:
         return 1
     pp = _VARIANT["name"] == "pp"   # 256x128 tiles, two resident blocks per CU
     tiles = (M // 256) * (N // (128 if pp else 256))
-    slots = NUM_CUS * (2 if pp else 1)
+    slots = num_cus() * (2 if pp else 1)
     if tiles >= slots * 0.75:
         return 1
 
@@ -226,18 +238,6 @@ def set_splitk(enabled: bool) -> bool:
 
 
 _VARIANT = {"name": "auto"}
-# The plain long-K NT store (the forward's second GEMM, y = a·W2ᵀ with K = F) is the one FFN GEMM where hipBLASLt's
-# kernel beats the native family (1570 vs 1481 TF isolated, profiles/r4/gemm_vs_hipblaslt_r4.txt; flagship step
-# 29.30-29.40 vs 29.46-29.67 ms, profiles/r4/fwd2_hipblaslt_r4.txt).  A caller opts in per call (``library=True``);
-# the engine does so for that GEMM on single-rank meshes only: under collectives that hold CUs hipBLASLt's
-# non-persistent grids lose 32-40 % (profiles/interference_r1.log) where the persistent native kernels lose nothing.
-# DLLM_NT_STORE_LIB=0 / 1 overrides the engine's choice.
-LIB_NT_STORE_ENV = os.environ.get("DLLM_NT_STORE_LIB")
-
-
-def lib_nt_store_default(single_rank: bool) -> bool:
-    """Whether an engine routes its forward's plain long-K NT store to hipBLASLt (``gemm(..., library=True)``)."""
-    return (LIB_NT_STORE_ENV == "1") if LIB_NT_STORE_ENV in ("0", "1") else bool(single_rank)
 # Launch policy of the 256x256 bf16 kernels (tiles per persistent block, minimum blocks per CU): Python-level
 # defaults that every call passes to the library explicitly -- the native side keeps no mutable state, so
 # GEMMs issued concurrently on different streams never race on a setting.
@@ -264,12 +264,10 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
          alpha: float = 1.0, beta: float = 0.0, out_dtype: torch.dtype | None = None, group_m: int | None = None,
          force: str | None = None, lr: float = 0.0, betas: tuple = (0.9, 0.95), eps: float = 1e-8,
          wd: float = 0.0, step: int = 0, opt_m: torch.Tensor | None = None,
-         opt_v: torch.Tensor | None = None, mask: torch.Tensor | None = None,
-         library: bool = False) -> torch.Tensor:
+         opt_v: torch.Tensor | None = None, mask: torch.Tensor | None = None) -> torch.Tensor:
     """``mask`` (ReLU only, GPU, see ``relu_mask_supported``): ``epi="act"`` also writes the activation-gradient
     bitmask, ``epi="dact"`` reads it instead of ``aux`` (1 bit instead of a bf16 per element).  CPU tensors
-    ignore it (``aux`` stays the source of truth there).  ``library``: a plain bf16 NT store with K >= 8192 runs
-    through hipBLASLt (see ``lib_nt_store_default``); any other GEMM ignores it."""
+    ignore it (``aux`` stays the source of truth there)."""
     M, N, K = gemm_shape(a, b, layout)
     if group_m is None:   # raster band height: the layout's policy (profiles/r3/group_m_sweep_r3.txt)
         group_m = _POLICY["group_m_nt"] if layout == "nt" else 4
@@ -308,10 +306,6 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
 
     for t, nm in ((a, "a"), (b, "b"), (out, "out")):
         _check_rowmajor(t, nm)
-    if (library and layout == "nt" and epi == "store" and mask is None and alpha == 1.0 and beta == 0.0
-            and a.dtype == torch.bfloat16 and out.dtype == torch.bfloat16 and K >= 8192 and force is None):
-        torch.matmul(a, b.t(), out=out)   # hipBLASLt (see lib_nt_store_default)
-        return out
     if (a.dtype == torch.float32 and mask is None and _use_bf16x6(M, N, K, force)
             and all(t.data_ptr() % 16 == 0 and t.stride(0) % 4 == 0 for t in (a, b))):
         # fp32-accurate GEMM on the bf16 matrix cores: split both operands into three bf16 parts and run one
@@ -380,7 +374,8 @@ def use_m224(M: int, N: int) -> bool:
 
     def fill(bm):
         t = (M // bm) * (N // 256)
-        return t / (-(-t // NUM_CUS) * NUM_CUS)
+        ncu = num_cus()
+        return t / (-(-t // ncu) * ncu)
 
     return fill(224) > fill(256)
 
@@ -404,11 +399,11 @@ def pair_supported(shapes, dtype: torch.dtype = torch.bfloat16, layout: str = "t
     if layout == "nn":
         if not (use_m224(M0, N0) and use_m224(M1, N1)):
             return False
-        return (M0 // 224) * (N0 // 256) + (M1 // 224) * (N1 // 256) <= NUM_CUS
+        return (M0 // 224) * (N0 // 256) + (M1 // 224) * (N1 // 256) <= num_cus()
     if any(m % 256 or n % 256 for m, n in ((M0, N0), (M1, N1))):
         return False
     tiles = (M0 // 256) * (N0 // 256) + (M1 // 256) * (N1 // 256)
-    return tiles <= NUM_CUS and (choose_ksplit(M0, N0, K0) > 1 or choose_ksplit(M1, N1, K1) > 1)
+    return tiles <= num_cus() and (choose_ksplit(M0, N0, K0) > 1 or choose_ksplit(M1, N1, K1) > 1)
 
 
 def gemm_pair(a0: torch.Tensor, b0: torch.Tensor, kw0: dict, a1: torch.Tensor, b1: torch.Tensor, kw1: dict,

@@ -118,6 +118,12 @@ def gpu_chunk_count(T: int, D: int, F_loc: int, R1: int, c: int) -> int:
 class FFNTrainer:
     def __init__(self, cfg: TrainConfig, mesh: Mesh, device: torch.device):
         self.cfg, self.mesh, self.device = cfg, mesh, torch.device(device)
+        if self.device.type == "cuda":
+            # before the engine's side streams exist: keep them off the compute stream's hardware queue (idempotent;
+            # bench.py / the launcher / init_distributed reserve earlier, before torch's stream pool exists)
+            from ..utils.streams import reserve_compute_queue
+
+            reserve_compute_queue(self.device)
         m = cfg.model
         D, F, L = m.D, m.F, m.layers
         t, d = mesh.tp, mesh.dp
@@ -157,10 +163,6 @@ class FFNTrainer:
                       and use_m224(self.F_loc, T) and use_m224(self.F_loc, D) and T % 256 == 0)
         self.step_count = 0
         dev = self.device
-        # the forward's plain long-K NT store through hipBLASLt, where no collective holds CUs (ops/gemm.py)
-        from ..ops.gemm import lib_nt_store_default
-
-        self.lib_fwd2 = dev.type == "cuda" and lib_nt_store_default(mesh.world == 1)
         if dev.type == "cuda":
             from ..ops.gemm import set_fp32_mode, set_min_blocks_per_cu, set_tiles_per_block
 
@@ -178,7 +180,10 @@ class FFNTrainer:
             comm.set_serialize(True)
         # custom xGMI all-reduce for the TP activation exchange (opt-in; gradients stay on RCCL)
         self.tp_car = None
-        if cfg.tp_allreduce == "custom" and t > 1 and self.device.type == "cuda" and not cfg.sequence_parallel:
+        self.tp_ar_choice = None
+        if cfg.tp_allreduce not in ("rccl", "custom", "auto"):
+            raise ValueError(f"tp_allreduce {cfg.tp_allreduce!r}: expected rccl | custom | auto")
+        if cfg.tp_allreduce in ("custom", "auto") and t > 1 and self.device.type == "cuda" and not cfg.sequence_parallel:
             from .car import CustomAllReduce
 
             # zero-copy: the exchanged activations (layer outputs xs[1..L], input gradients dxb) live in the car's
@@ -187,7 +192,13 @@ class FFNTrainer:
             per = (cfg.tokens * D * es + 255) // 256 * 256
             self.tp_car = CustomAllReduce(mesh.tp_ranks, self.device, cap_bytes=4096, tag=f"tp{mesh.dp_rank}",
                                           arena_bytes=(L + 3) * per)
-            mesh.groups["tp_car"] = self.tp_car
+            if cfg.tp_allreduce == "auto":
+                self.tp_ar_choice = self._choose_tp_allreduce(cfg.tokens, D)
+                if self.tp_ar_choice["choice"] == "rccl":
+                    self.tp_car.destroy()
+                    self.tp_car = None
+            if self.tp_car is not None:
+                mesh.groups["tp_car"] = self.tp_car
 
         # ---- flat owned parameter layout (completion order) ------------------------------------
         full = {"w2": (self.F_loc, D) if self.tmode else (D, self.F_loc), "w1": (self.R1, D)}
@@ -240,12 +251,16 @@ class FFNTrainer:
         no_coll = not (self.ddp or self.fsdp or self.zero)
         # side-stream optimizer: wgrad GEMMs store the gradient, a low-occupancy SGD kernel on its own
         # stream updates the weight while the next GEMMs run; the forward waits per weight
-        self.side_opt = (no_coll and cfg.side_optimizer > 0 and cfg.optimizer == "sgd" and dev.type == "cuda")
+        # SGD: fp32 master (dllm_sgd_step_stream); AdamW (round 5): split master, the 24 B/param of
+        # master + moments streamed by adam_split_kernel on at most side_optimizer workgroups
+        self.side_opt = (no_coll and cfg.side_optimizer > 0 and dev.type == "cuda" and
+                         (cfg.optimizer == "sgd" or (cfg.optimizer == "adam" and cfg.master == "split"
+                                                     and self.cd == torch.bfloat16)))
         # Split master (bf16 SGD): the fp32 master is the bf16 working copy (hi) plus an int16 residual plane (lo),
         # bitwise the same fp32 values (ops/master.py).  4 B/param of weight state instead of 6 B, and every update
         # (fused wgrad epilogue or flat kernel) reads 4 B and writes 4 B per parameter instead of 4 B + 6 B.
         nmaster = self.shard_total if self.zero else self.total
-        self.split = cfg.master == "split" and self.cd == torch.bfloat16 and not self.side_opt
+        self.split = cfg.master == "split" and self.cd == torch.bfloat16 and (not self.side_opt or cfg.optimizer == "adam")
         if cfg.master not in ("split", "fp32"):
             raise ValueError(f"unknown master format {cfg.master!r}")
         self._master = None if self.split else torch.zeros(nmaster, dtype=torch.float32, device=dev)
@@ -268,7 +283,7 @@ class FFNTrainer:
             # write the working copy in place and the gradient GEMMs write the shard gradient directly -- size-1
             # collectives that move nothing (RCCL launches no kernel), the degenerate case of the N-rank schedule
             # (every wait, event and stream edge is still issued).  dp > 1: 2-slot gather / gradient rings.
-            self.fsdp_alias = d == 1
+            self.fsdp_alias = d == 1 and cfg.fsdp_alias
             self.wring = [{n: torch.empty(0 if self.fsdp_alias else full[n], dtype=self.cd, device=dev)
                            for n in ("w2", "w1")} for _ in range(2)]
             self.gring = [{n: torch.empty(0 if self.fsdp_alias else full[n], dtype=self.gd, device=dev)
@@ -573,6 +588,50 @@ class FFNTrainer:
         return out
 
     @torch.no_grad()
+    def _choose_tp_allreduce(self, T: int, D: int, iters: int = 5, warm: int = 2) -> dict:
+        """``tp_allreduce="auto"``: time RCCL (the tp role communicator) against the custom peer all-reduce
+        (``csrc/car.hip``, zero-copy arena) on the TP message itself, ``[T, D]`` in the compute dtype, on the real tp
+        group; the faster one carries the activation exchange.  Both timings are the max over the tp ranks, so every
+        rank makes the same choice.  Bandwidths: algorithm = bytes / time, bus = 2(n-1)/n x algorithm (ring
+        convention).  A few ms at 64 MiB on xGMI (budget: well under 0.5 s)."""
+        n = self.mesh.tp
+        x = self.tp_car.arena_view((T, D), self.cd)   # the arena's first range (released below: xs[1] reuses it)
+        x.normal_()
+        nbytes = x.numel() * x.element_size()
+        grp = self.mesh.group("tp")
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+
+        def timed(fn):
+            for _ in range(warm):
+                fn()
+            ev[0].record()
+            for _ in range(iters):
+                fn()
+            ev[1].record()
+            torch.cuda.synchronize(self.device)
+            return ev[0].elapsed_time(ev[1]) / iters
+
+        t_rccl = timed(lambda: comm.all_reduce(x, grp, async_op=False))
+        t_car = timed(lambda: self.tp_car.all_reduce(x))
+        self.tp_car.check()
+        self.tp_car._arena_next = 0
+        tt = torch.tensor([t_rccl, t_car], dtype=torch.float64, device=self.device)
+        if grp is not None:
+            import torch.distributed as dist
+
+            if isinstance(grp, dist.ProcessGroup):
+                dist.all_reduce(tt, op=dist.ReduceOp.MAX, group=grp)
+            else:   # native communicator: MAX over the tp ranks through the default group
+                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_rccl, t_car = float(tt[0]), float(tt[1])
+
+        def bw(ms):
+            alg = nbytes / (ms * 1e-3) / 1e9
+            return {"ms": round(ms, 4), "algbw_GBps": round(alg, 1), "busbw_GBps": round(alg * 2 * (n - 1) / n, 1)}
+
+        return {"choice": "custom" if t_car < t_rccl else "rccl", "bytes": nbytes, "ranks": n,
+                "rccl": bw(t_rccl), "custom": bw(t_car)}
+
     def load_full_params(self, layers: list[dict], flat: torch.Tensor | None = None) -> None:
         """Set parameters (or another flat state buffer) from full logical tensors (identical on every
         rank; CPU or device)."""
@@ -742,9 +801,15 @@ class FFNTrainer:
             st = self.opt_stream_side
             st.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(st):
-                copy = None if self.shared_copy else self.copy[s_:e_]
-                sgd_step_(self._master[s_:e_], self.grads[s_:e_], self.cfg.lr, copy=copy,
-                          max_blocks=self.cfg.side_optimizer)
+                if self.split:   # AdamW on the split master (the bf16 working copy is its high half)
+                    c = self.cfg
+                    adam_split_step_(self.master_lo[s_:e_], self.copy[s_:e_], self.grads[s_:e_], self.adam_m[s_:e_],
+                                     self.adam_v[s_:e_], self.step_count, c.lr, c.adam_b1, c.adam_b2, c.adam_eps,
+                                     c.weight_decay, max_blocks=c.side_optimizer)
+                else:
+                    copy = None if self.shared_copy else self.copy[s_:e_]
+                    sgd_step_(self._master[s_:e_], self.grads[s_:e_], self.cfg.lr, copy=copy,
+                              max_blocks=self.cfg.side_optimizer)
                 ev = torch.cuda.Event()
                 ev.record(st)
             self.opt_done[(l, name)] = ev
@@ -1022,7 +1087,7 @@ class FFNTrainer:
                     layer_fwd_t(self.xs[l], w1, w2, act, a, h, self.xs[l + 1], before_fwd2=before2, mask=self._mask(l))
                 else:
                     layer_fwd(self.xs[l], w1, w2, act, gated, a, h, self.xs[l + 1], before_fwd2=before2,
-                              mask=self._mask(l), library_fwd2=self.lib_fwd2)
+                              mask=self._mask(l))
                 if self.tp_comm:
                     last = l == L - 1
                     if self.tp_car is not None:

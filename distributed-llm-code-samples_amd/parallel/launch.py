@@ -69,6 +69,14 @@ def run_rank(rank: int, world: int, cfg_dict: dict, method: int, backend: str, p
     # opts["device"] == "cuda" with gloo: several ranks share one GPU (RCCL refuses two ranks on one device), so
     # the multi-rank engine paths run with the HIP kernels and streams, collectives staged through the host
     use_gpu = backend == "nccl" or opts.get("device") == "cuda"
+    if use_gpu:
+        # keep every later stream (torch's pool: engine side streams, process-group streams) off the compute stream's
+        # hardware queue, on every GPU path incl. world == 1 and gloo-on-cuda ranks (init_distributed does it for
+        # nccl); before anything creates streams
+        from ..utils.streams import reserve_compute_queue
+
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", rank)) % max(1, torch.cuda.device_count()))
+        reserve_compute_queue(torch.cuda.current_device())
     if world > 1 or opts.get("force_dist"):
         init_distributed(backend, rank, world, "127.0.0.1", port)
     device = torch.device("cuda", torch.cuda.current_device()) if use_gpu else torch.device("cpu")

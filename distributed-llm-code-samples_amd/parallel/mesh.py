@@ -70,6 +70,8 @@ class Mesh:
     dp_ranks: list = field(default_factory=list)
     tp_ranks: list = field(default_factory=list)
     native_world: object = None  # native backend: the communicator the role communicators are split from
+    # the HIP stream each role communicator runs on ({role: raw handle}, None = not identified); see _queue_plan
+    role_streams: dict = field(default_factory=dict)
 
     @property
     def world(self) -> int:
@@ -129,6 +131,16 @@ class Mesh:
         m.tp_ranks = [m.dp_rank * tp + t for t in range(tp)]
         if not dist.is_initialized() or (world == 1 and not force):
             return m
+        # Distinct hardware queues per role: the FSDP gather and reduce-scatter must not share
+        # one, or the reference's serialisation (train_ffns.py:14, :252) just moves down to the queue; no role may
+        # share the compute stream's.  ``avoid[role]`` = the roles whose streams its stream must not queue with.
+        on_gpu = device is not None and device.type == "cuda" and os.environ.get("DLLM_ROLE_QUEUES", "1") != "0"
+        avoid = {"dp_ar": ["compute"], "dp_ag": ["compute"], "dp_rs": ["compute", "dp_ag"], "tp": ["compute"]}
+
+        def handles(role):
+            return [0 if r == "compute" else m.role_streams.get(r) for r in avoid[role]
+                    if r == "compute" or m.role_streams.get(r)]
+
         if comm_backend == "native":
             # one job-wide RCCL communicator (store-bootstrapped uniqueId), then every role communicator is
             # ncclCommSplit from it: color = this rank's dp group (dp roles) or tp group (tp role), key = its
@@ -147,8 +159,32 @@ class Mesh:
                 if not separate_streams and role in ("dp_ag", "dp_rs") and "dp_ar" in m.groups:
                     m.groups[role] = m.groups["dp_ar"]
                     continue
-                m.groups[role] = NativeGroup.split(world_comm, tp_groups if role == "tp" else dp_groups, dev)
+                m.groups[role] = NativeGroup.split(world_comm, tp_groups if role == "tp" else dp_groups, dev,
+                                                   avoid=handles(role) if on_gpu else None)
+                if m.groups[role] is not None:
+                    m.role_streams[role] = m.groups[role].stream
             return m
+        cursor = None
+        if on_gpu and dist.get_backend() == "nccl":
+            from ..utils.streams import PoolCursor
+
+            cursor = PoolCursor(device)
+
+        def new_group(ranks, role):
+            """dist.new_group + (nccl, GPU) steer torch's stream pool so the communicator's stream lands on an allowed
+            queue, then identify the stream it took (a 1-element all-reduce makes sure the communicator exists)."""
+            member = rank in ranks
+            if cursor is not None and member:
+                cursor.steer(handles(role))
+            g = dist.new_group(ranks)
+            if cursor is not None and member:
+                t = torch.zeros(1, device=device)
+                dist.all_reduce(t, group=g)
+                torch.cuda.synchronize(device)
+                st = cursor.taken()
+                m.role_streams[role] = st.cuda_stream if st is not None else None
+            return g
+
         # every rank creates every group in the same order (new_group is collective)
         for role in ROLES:
             if role.startswith("dp"):
@@ -158,13 +194,13 @@ class Mesh:
                     m.groups[role] = m.groups["dp_ar"]
                     continue
                 if dp == world:
-                    grp = dist.new_group(list(range(world)))
+                    grp = new_group(list(range(world)), role)
                     m.groups[role] = grp
                 else:
                     mine = None
                     for t in range(tp):
                         ranks = [d * tp + t for d in range(dp)]
-                        g = dist.new_group(ranks)
+                        g = new_group(ranks, role)
                         if rank in ranks:
                             mine = g
                     m.groups[role] = mine
@@ -172,12 +208,12 @@ class Mesh:
                 if tp == 1 and not force:
                     continue
                 if tp == world:
-                    m.groups[role] = dist.new_group(list(range(world)))
+                    m.groups[role] = new_group(list(range(world)), role)
                 else:
                     mine = None
                     for d in range(dp):
                         ranks = [d * tp + t for t in range(tp)]
-                        g = dist.new_group(ranks)
+                        g = new_group(ranks, role)
                         if rank in ranks:
                             mine = g
                     m.groups[role] = mine

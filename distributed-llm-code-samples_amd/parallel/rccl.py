@@ -108,7 +108,7 @@ class NativeGroup:
     of a parent communicator with ``ncclCommSplit`` (``NativeGroup.split``, how 2-D meshes are built)."""
 
     def __init__(self, ranks: list[int], tag: str, device: torch.device, store=None, priority: int = 0,
-                 _comm: int | None = None):
+                 _comm: int | None = None, avoid: list | None = None):
         self.ranks = list(ranks)
         me = dist.get_rank()
         if me not in self.ranks:
@@ -131,12 +131,19 @@ class NativeGroup:
                    "ncclCommInitRank")
             _comm = comm.value
         self.comm = _comm
-        st = ctypes.c_void_p()
-        _check(_lib().dllm_stream_create(priority, ctypes.byref(st)), "hipStreamCreate")
-        self.stream = st.value
+        if avoid is not None:
+            # a stream on a hardware queue none of ``avoid`` (stream handles; 0 = compute) uses (utils/streams.py)
+            from ..utils.streams import create_stream_off
+
+            self.stream = create_stream_off(device, avoid, priority)
+        else:
+            st = ctypes.c_void_p()
+            _check(_lib().dllm_stream_create(priority, ctypes.byref(st)), "hipStreamCreate")
+            self.stream = st.value
 
     @classmethod
-    def split(cls, parent: "NativeGroup", groups: list[list[int]], device: torch.device) -> "NativeGroup | None":
+    def split(cls, parent: "NativeGroup", groups: list[list[int]], device: torch.device,
+              avoid: list | None = None) -> "NativeGroup | None":
         """``ncclCommSplit`` of ``parent`` into ``groups`` (lists of global ranks, disjoint): collective over
         ALL of the parent's ranks; returns this rank's new group (its own communicator and stream), or None
         if this rank is in none of them (it passes NCCL_SPLIT_NOCOLOR)."""
@@ -150,7 +157,7 @@ class NativeGroup:
                "ncclCommSplit")
         if mine is None:
             return None
-        return cls(mine, "split", device, _comm=comm.value)
+        return cls(mine, "split", device, _comm=comm.value, avoid=avoid)
 
     def size(self) -> int:
         return self._size

@@ -84,11 +84,14 @@ class TrainConfig:
     side_optimizer: int = 0          # >0 (no grad collective, SGD): wgrad GEMMs store grads and a side stream
                                      # applies SGD on this many workgroups, overlapped with the next GEMMs
     force_comm: bool = False         # run the DDP/FSDP collective path even at dp=1 (single-GPU RCCL check)
+    fsdp_alias: bool = True          # FSDP at dp = 1: gathers / gradient writes alias the full buffers (size-1
+                                     # collectives move nothing); False: the dp > 1 rings + real copying collectives
     force_tp_comm: bool = False      # with force_comm: also run the TP/SP collectives (forward output all-reduce
                                      # in chunks, deferred last-layer all-reduce, dx all-reduce / SP reduce-scatter
                                      # and all-gathers) over the size-1 tp communicator (single-GPU RCCL check)
     comm_backend: str = "torch"      # torch (ProcessGroupNCCL/gloo) | native (csrc/comm.cpp RCCL layer)
-    tp_allreduce: str = "rccl"       # TP activation all-reduce: rccl (role communicator) | custom (csrc/car.hip)
+    tp_allreduce: str = "rccl"       # TP activation all-reduce: rccl (role communicator) | custom (csrc/car.hip) |
+                                     # auto (time both on the [T, D] message at engine build, keep the faster)
     debug_sync: bool = False         # race screen: wait every collective at issue + device sync per layer
     master: str = "split"            # fp32 master weights of a bf16 run: split (the bf16 working copy + an int16
                                      # residual plane, together exactly the fp32 master: 4 B/param of weight state,
@@ -133,7 +136,7 @@ def add_extended_args(p: argparse.ArgumentParser) -> None:
     p.add_argument("--backend", choices=["auto", "nccl", "rccl", "gloo"], default="auto")
     p.add_argument("--comm", choices=["torch", "native"], default="torch",
                    help="communicator implementation for the role groups (native = C++ RCCL layer)")
-    p.add_argument("--tp_allreduce", choices=["rccl", "custom"], default="rccl",
+    p.add_argument("--tp_allreduce", choices=["rccl", "custom", "auto"], default="rccl",
                    help="TP activation all-reduce: RCCL or the custom two-shot xGMI peer all-reduce")
     p.add_argument("--nprocs", type=int, default=0, help="ranks to spawn (0 = all visible GPUs)")
     p.add_argument("--dp", type=int, default=0)

@@ -142,6 +142,128 @@ def shares_compute_queue(stream: torch.cuda.Stream, device=None, tries: int = 3)
     return 2 * votes > tries
 
 
+def shares_queue(a: int | None, b: int | None, device=None, tries: int = 3) -> bool:
+    """Whether raw HIP streams ``a`` and ``b`` (handles; None / 0 = the null, i.e. compute, stream) run on one hardware
+    queue (measured; majority of ``tries`` probes; synchronises both).  ``a`` spins, then ``b`` stamps: a shared queue
+    runs them in order."""
+    if (a or 0) == (b or 0):
+        return True
+    votes = 0
+    with torch.cuda.device(_index(device)):
+        for _ in range(tries):
+            r = _native.lib().dllm_queue_shared(ctypes.c_void_p(a or None), ctypes.c_void_p(b or None), PROBE_SPIN_US)
+            if r < 0:
+                raise RuntimeError(f"dllm_queue_shared failed ({r})")
+            votes += r
+    return 2 * votes > tries
+
+
+_QUEUE_BLOCKERS: dict[int, list[int]] = {}
+
+
+def create_stream_off(device, avoid: list, priority: int = 0, max_tries: int = 16) -> int:
+    """A new native stream (handle) on a hardware queue that none of the ``avoid`` streams (handles; 0 = compute) uses.
+    Candidates that land on an avoided queue are kept for the process as blockers -- they raise that queue's use
+    count, so HIP's least-used placement puts the next candidate elsewhere (the compute-queue reservation's
+    mechanism).  After ``max_tries`` the last candidate is returned as is (``role_queue_report`` then shows the
+    conflict)."""
+    idx = _index(device)
+    blockers = _QUEUE_BLOCKERS.setdefault(idx, [])
+    h = None
+    for _ in range(max_tries):
+        st = ctypes.c_void_p()
+        with torch.cuda.device(idx):
+            rc = _native.lib().dllm_stream_create(int(priority), ctypes.byref(st))
+            if rc != 0 or not st.value:
+                raise RuntimeError(f"hipStreamCreateWithPriority failed ({rc})")
+            h = st.value
+            # first use acquires the queue: not part of the timed probes
+            _native.lib().dllm_queue_shared(ctypes.c_void_p(h), ctypes.c_void_p(h), 0)
+        if not any(shares_queue(a, h, idx) for a in avoid):
+            return h
+        blockers.append(h)
+    return h
+
+
+class PoolCursor:
+    """torch's per-device pool of normal-priority streams, as an ordered ring with a known position.
+
+    ``torch.cuda.Stream()`` and ProcessGroupNCCL's collective streams (``at::cuda::getStreamFromPool``) are handed out
+    round-robin from one per-device counter over 32 streams.  Walking the ring once gives its order and the counter's
+    position, so the stream the NEXT process group will take is known (``peek``), can be skipped when it sits on an
+    unwanted hardware queue (``skip``), and what a group creation actually took is checked afterwards (``taken``)."""
+
+    def __init__(self, device):
+        self.idx = _index(device)
+        first = torch.cuda.Stream(device=self.idx)
+        ring = [first]
+        while True:
+            st = torch.cuda.Stream(device=self.idx)
+            if st.cuda_stream == first.cuda_stream:
+                break
+            ring.append(st)
+            if len(ring) > 256:
+                raise RuntimeError("torch stream pool is not a ring")
+        self.ring = ring
+        self.pos = 1 % len(ring)   # ``first`` was handed out twice: the counter now points past it
+
+    def peek(self) -> torch.cuda.Stream:
+        return self.ring[self.pos]
+
+    def skip(self) -> None:
+        torch.cuda.Stream(device=self.idx)
+        self.pos = (self.pos + 1) % len(self.ring)
+
+    def taken(self) -> torch.cuda.Stream | None:
+        """After something drew from the pool: if it drew exactly one stream (the one ``peek`` showed), return it
+        (the cursor moves past it and past this check's own draw), else None (cursor resynchronised)."""
+        expect = self.ring[self.pos]
+        st = torch.cuda.Stream(device=self.idx)
+        n = len(self.ring)
+        at = next(i for i in range(n) if self.ring[i].cuda_stream == st.cuda_stream)
+        took = (at - self.pos) % n
+        self.pos = (at + 1) % n
+        return expect if took == 1 else None
+
+    def steer(self, avoid: list, max_skips: int = 32) -> torch.cuda.Stream:
+        """Skip pool streams until the next one shares no hardware queue with ``avoid`` (handles; 0 = compute)."""
+        for _ in range(max_skips):
+            if not any(shares_queue(a, self.peek().cuda_stream, self.idx) for a in avoid):
+                break
+            self.skip()
+        return self.peek()
+
+
+# role pairs that must not share a hardware queue: any communicator role with the compute stream, and the FSDP
+# gather with the FSDP reduce-scatter (the reference's serialisation, train_ffns.py:14, :252-256)
+MUST_DIFFER = (("compute", "dp_ag"), ("compute", "dp_rs"), ("compute", "dp_ar"), ("compute", "tp"),
+               ("dp_ag", "dp_rs"))
+
+
+def role_queue_report(device, named: dict) -> dict:
+    """Pairwise hardware-queue sharing among ``named`` streams ({name: handle or stream}; "compute" = the null stream
+    is added; None entries are reported as unknown).  ``role_queue_conflicts``: the ``MUST_DIFFER`` pairs (plus every
+    stream against compute) that share a queue."""
+    idx = _index(device)
+    h = {"compute": 0}
+    unknown = []
+    for n, st in named.items():
+        if st is None:
+            unknown.append(n)
+            continue
+        h[n] = st if isinstance(st, int) else st.cuda_stream
+    names = list(h)
+    sharing = []
+    for i in range(len(names)):
+        for j in range(i + 1, len(names)):
+            a, b = names[i], names[j]
+            if shares_queue(h[a], h[b], idx):
+                sharing.append([a, b])
+    must = {tuple(p) for p in MUST_DIFFER} | {("compute", n) for n in names if n != "compute"}
+    conflicts = [p for p in sharing if tuple(p) in must or tuple(p[::-1]) in must]
+    return {"role_queue_conflicts": conflicts, "queue_sharing_pairs": sharing, "unknown_streams": unknown}
+
+
 def queue_report(device, streams: dict, pool: bool = True) -> dict:
     """Which of ``streams`` ({name: stream}, None entries skipped) -- plus, with ``pool``, torch's 32 normal-priority
     pool streams, which ProcessGroupNCCL's collective streams come from -- share the compute stream's hardware queue.

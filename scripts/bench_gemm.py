@@ -44,6 +44,10 @@ def main():
                          "'dyn' = dynamic persistent blocks")
     ap.add_argument("--cases", default="", help="comma-separated substrings selecting cases")
     ap.add_argument("--no_torch", action="store_true")
+    ap.add_argument("--libs", default="",
+                    help="comma-separated alternate native builds (python -m dllm._build --variant NAME -D...): each "
+                         "becomes variant 'libI' (production kernels, tpb 8), timed interleaved with the others, and its "
+                         "outputs are checked bitwise against the first variant's")
     a = ap.parse_args()
     T, D, F = a.T, a.D, a.F
     bf = torch.bfloat16
@@ -61,6 +65,7 @@ def main():
     gw2 = torch.empty(D, F, device=dev, dtype=torch.float32)
     mw2 = torch.randn(D, F, device=dev, dtype=torch.float32) * 0.02   # fp32 master + bf16 copy (fused SGD)
     cw2 = mw2.to(bf)
+    rw2 = torch.zeros(D, F, device=dev, dtype=torch.int16)   # split master: bf16 copy + int16 residual plane
     gm = a.group_m
     cases = {
         "fwd1 h=x.W1t (NT,act)": (lambda: gemm(x, w1, "nt", out=act, epi="act", act="relu", group_m=gm),
@@ -70,6 +75,8 @@ def main():
                                lambda: (dy.t() @ h).float()),
         "dW2 sgd (TN,fused)": (lambda: gemm(dy, h, "tn", out=mw2, epi="sgd", lr=1e-9, aux_out=cw2, group_m=gm),
                                lambda: mw2.add_((dy.t() @ h).float(), alpha=-1e-9)),
+        "dW2 sgd_split (TN,fused)": (lambda: gemm(dy, h, "tn", out=rw2, epi="sgd_split", lr=1e-9, aux_out=cw2,
+                                                  group_m=gm), lambda: mw2.add_((dy.t() @ h).float(), alpha=-1e-9)),
         "da=dy.W2 (NN,dact)": (lambda: gemm(dy, w2, "nn", out=da, epi="dact", act="relu", aux=h, group_m=gm),
                                lambda: (dy @ w2) * (h > 0)),
         "dx=da.W1 (NN)": (lambda: gemm(h, w1, "nn", out=dx, group_m=gm), lambda: h @ w1),
@@ -77,15 +84,50 @@ def main():
     }
     flops = 2 * T * D * F
     variants = a.variants.split(",")
+    libs = {}
+    if a.libs:
+        from dllm import _native
+        base = _native.lib()
+        for i, path in enumerate(a.libs.split(",")):
+            os.environ["DLLM_NATIVE_LIB"] = path
+            libs[f"lib{i}"] = _native._load()
+        os.environ.pop("DLLM_NATIVE_LIB")
+        libs["lib_base"] = base
+        variants = ["lib_base"] + sorted(k for k in libs if k != "lib_base")
+        state = [mw2, cw2, rw2]
+        outs = {"fwd1": act, "fwd2": y, "dW2=": gw2, "dW2 sgd ": mw2, "dW2 sgd_split": rw2, "da=": da, "dx=": dx,
+                "dW1=": gw1}
     res = {}
     if a.cases:
         cases = {k: v for k, v in cases.items() if any(c in k for c in a.cases.split(","))}
     for name, (mine, ref) in cases.items():
         times = {v: [] for v in variants}
+        if libs:   # bitwise check of every build against the first, from the same initial state
+            init = [t.clone() for t in state]
+            got = {}
+            for v in variants:
+                for t, t0 in zip(state, init):
+                    t.copy_(t0)
+                _native._LIB = libs[v]
+                set_bf16_variant("8phase_stagger")
+                set_tiles_per_block(8)
+                mine()
+                torch.cuda.synchronize()
+                o = next(t for k, t in outs.items() if name.startswith(k))
+                got[v] = o.clone()
+                if name.startswith("dW2 sgd_split"):
+                    got[v] = torch.cat([o.view(torch.int16).flatten(), cw2.view(torch.int16).flatten()])
+            for v in variants[1:]:
+                same = torch.equal(got[v].view(torch.uint8), got[variants[0]].view(torch.uint8))
+                print(f"  bitwise {v} == {variants[0]}: {same}", flush=True)
         tr = []
         for _ in range(a.rounds):  # interleaved rounds in one process (guide §5.4 rule 24)
             for v in variants:
-                if v.startswith("tpb"):
+                if v in libs:
+                    _native._LIB = libs[v]
+                    set_bf16_variant("8phase_stagger")
+                    set_tiles_per_block(8)
+                elif v.startswith("tpb"):
                     set_bf16_variant("8phase_stagger")
                     set_tiles_per_block(int(v[3:]))
                 elif v.startswith("pp"):   # 256x128 two-blocks-per-CU family; ppN[sK]: N tiles per persistent
@@ -112,6 +154,8 @@ def main():
         print(msg, flush=True)
     set_bf16_variant("auto")
     set_tiles_per_block(8)
+    if libs:
+        _native._LIB = libs["lib_base"]
     if a.json:
         with open(a.json, "w") as f:
             json.dump({"T": T, "D": D, "F": F, "cases": res}, f, indent=1)

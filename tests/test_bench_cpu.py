@@ -41,10 +41,13 @@ def test_bench_methods_side_by_side(free_port):
     (the reference's --method 0, train_ffns.py:373-384; hybrid = BASELINE config 5, FSDP x TP on a SwiGLU stack)."""
     rec = _run(free_port)
     assert rec["config"]["parallelism"] == "dp2-zero2" and rec["config"]["global_batch"] == 4
-    assert set(rec["methods"]) == {"ddp", "zero", "fsdp", "tp", "hybrid"}
+    assert set(rec["methods"]) == {"ddp", "zero", "fsdp", "tp", "hybrid"}   # fsdp_copy: N = 1 only
     for name, m in rec["methods"].items():
         assert m["value"] > 0 and m["ms_per_step"] > 0 and m["finite"], name
         assert {"peak_hbm_gib", "parallelism", "model", "state_gib"} <= set(m), name
+        # steady-state windows: >= 150 ms of warm-up and ~300 ms timed (or the step cap); the timed window is sized
+        # from the warm step time, which reads noisy on shared CPU cores (the GPU runs check >= 300 ms)
+        assert m["warmup_ms"] >= 150 and (m["timed_ms"] >= 200 or m["steps"] >= 1000), (name, m)
     assert rec["methods"]["tp"]["parallelism"] == "tp2" and "L1 D64 F128" in rec["methods"]["tp"]["model"]
     assert rec["methods"]["fsdp"]["parallelism"] == "fsdp2"
     assert rec["methods"]["hybrid"]["parallelism"] == "fsdp1xtp2" and "L2 D64 F128 swiglu-silu" in rec["methods"]["hybrid"]["model"]

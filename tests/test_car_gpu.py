@@ -75,7 +75,7 @@ def test_processes_ipc(n, dtype, arena, free_port):
     assert all(res.values()), res
 
 
-def _tp_proc(rank, n, port, q):
+def _tp_proc(rank, n, port, q, mode="custom"):
     import torch.distributed as dist
 
     from dllm.models.ffn import init_ffn_layer
@@ -93,25 +93,35 @@ def _tp_proc(rank, n, port, q):
     layers = [init_ffn_layer(D, F, gen) for _ in range(L)]
     batches = list(reference_mock_data(torch.randint(100_000, (3,), generator=gen), T, D))
     cfg = TrainConfig(model=ModelConfig(D, F, L), batch_size=1, seq_len=T, dtype="fp32", grad_dtype="fp32",
-                      lr=1e-2, dp=1, tp=n, tp_allreduce="custom", skip_input_grad=False)
+                      lr=1e-2, dp=1, tp=n, tp_allreduce=mode, skip_input_grad=False)
     mesh = Mesh.build(1, n, device=dev)
     eng = FFNTrainer(cfg, mesh, dev)
-    assert eng.tp_car is not None and eng.tp_car.arena is not None
-    assert eng.tp_car._arena_offset(eng.xs[1]) is not None and eng.tp_car._arena_offset(eng.dxb[0]) is not None
+    if mode == "auto":   # both timed on the [T, D] message; every rank made the same choice
+        ch = eng.tp_ar_choice
+        assert ch["choice"] in ("rccl", "custom") and ch["rccl"]["ms"] > 0 and ch["custom"]["ms"] > 0, ch
+        assert ch["bytes"] == T * D * 4 and ch["ranks"] == n
+        assert (eng.tp_car is not None) == (ch["choice"] == "custom")
+    if eng.tp_car is not None:
+        assert eng.tp_car.arena is not None
+        assert eng.tp_car._arena_offset(eng.xs[1]) is not None and eng.tp_car._arena_offset(eng.dxb[0]) is not None
     eng.load_full_params(layers)
     for x, dy in batches:
         eng.train_step(x.to(dev), dy.to(dev))
-    eng.tp_car.check()
+    if eng.tp_car is not None:
+        eng.tp_car.check()
     loc = [{k: v.cpu() for k, v in p.items()} for p in eng.local_params()]
-    q.put((rank, loc))
+    q.put((rank, (loc, eng.tp_ar_choice)))
     dist.barrier()
     mesh.destroy()
     dist.destroy_process_group()
 
 
-def test_tp_engine_with_custom_allreduce(free_port):
+@pytest.mark.parametrize("mode", ["custom", "auto"])
+def test_tp_engine_with_custom_allreduce(mode, free_port):
     """TP=2 training (two processes on the GPU, gloo only as the store) with the custom all-reduce for
-    the activation exchange equals single-device training up to reduction order (train_ffns.py:290-312)."""
+    the activation exchange equals single-device training up to reduction order (train_ffns.py:290-312).
+    ``auto``: the engine times the gloo tp group against the custom all-reduce on the [T, D] message and keeps the
+    faster (the gloo_gpu rehearsal of the 8-GPU selection; both ranks must agree)."""
     from dllm.models import reference as R
     from dllm.models.ffn import init_ffn_layer
     from dllm.utils.data import reference_mock_data
@@ -119,13 +129,16 @@ def test_tp_engine_with_custom_allreduce(free_port):
     n = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_tp_proc, args=(r, n, free_port, q)) for r in range(n)]
+    ps = [ctx.Process(target=_tp_proc, args=(r, n, free_port, q, mode)) for r in range(n)]
     for p in ps:
         p.start()
-    res = dict(q.get(timeout=240) for _ in range(n))
+    got = dict(q.get(timeout=240) for _ in range(n))
     for p in ps:
         p.join(60)
     assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+    res = {r: v[0] for r, v in got.items()}
+    if mode == "auto":
+        assert got[0][1]["choice"] == got[1][1]["choice"], got[0][1]
     D, F, L, T = 256, 1024, 2, 512
     gen = torch.Generator().manual_seed(7)
     layers = [init_ffn_layer(D, F, gen) for _ in range(L)]

@@ -79,14 +79,14 @@ def test_native_abort_error_path(pg):
     assert not mesh.groups
 
 
-def _run(dp_mode, backend, dtype="fp32", opt="sgd", force=True):
+def _run(dp_mode, backend, dtype="fp32", opt="sgd", force=True, fsdp_alias=True):
     D, F, L, T = 256, 1024, 2, 512
     gen = torch.Generator().manual_seed(9)
     layers = [init_ffn_layer(D, F, gen) for _ in range(L)]
     batches = list(reference_mock_data(torch.randint(100_000, (3,), generator=gen), T, D))
     cfg = TrainConfig(model=ModelConfig(D, F, L), batch_size=1, seq_len=T, dtype=dtype, grad_dtype="fp32",
                       lr=1e-2 if opt == "sgd" else 1e-3, optimizer=opt, dp_mode=dp_mode, force_comm=force,
-                      comm_backend=backend)
+                      comm_backend=backend, fsdp_alias=fsdp_alias)
     dev = torch.device("cuda", 0)
     mesh = Mesh.build(1, 1, force=force, comm_backend=backend, device=dev)
     eng = FFNTrainer(cfg, mesh, dev)
@@ -108,6 +108,17 @@ def test_dp_paths_match_single_device(pg, backend, dp_mode, opt):
     for g, w in zip(got, ref):
         for k in w:
             torch.testing.assert_close(g[k], w[k], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("backend", ["torch", "native"])
+def test_fsdp_copying_rings_equal_aliased(pg, backend):
+    """bench.py's fsdp_copy entry: FSDP at dp = 1 on its gather / gradient rings with real (copying) size-1 RCCL
+    all-gathers and reduce-scatters gives bitwise the aliased schedule's parameters."""
+    a = _run("fsdp", backend, dtype="bf16")
+    b = _run("fsdp", backend, dtype="bf16", fsdp_alias=False)
+    for g, w in zip(a, b):
+        for k in w:
+            assert torch.equal(g[k], w[k]), k
 
 
 @pytest.mark.parametrize("backend", ["torch", "native"])

@@ -78,3 +78,22 @@ def test_overlapped_equals_serialized(method, free_port):
     over = _run(_cfg(1024, 4096, 2, 2048, **base), method, 2, free_port)
     ser = _run(_cfg(1024, 4096, 2, 2048, debug_sync=True, **base), method, 2, free_port + 1)
     assert _equal(over, ser)
+
+
+def test_tp_transposed_layout_two_ranks_and_checkpoint_crossing(free_port, tmp_path):
+    """the transposed-activation TP layout (tmode: W2 stored transposed, 224-row tiles, NN fused optimizer)
+    on a real 2-rank TP group (gloo on cuda:0), F_loc = 1792.  Its masters match the row-major layout's after the same
+    steps, and a sharded checkpoint written by one layout resumes in the other (both directions)."""
+    base = dict(dtype="bf16", grad_dtype="bf16", lr=1e-3)
+    D, F, L, T = 256, 3584, 2, 512                 # F / tp = 1792 = 8 x 224 -> tmode
+    t_on = _cfg(D, F, L, T, tp_transposed=True, **base)
+    t_off = _cfg(D, F, L, T, tp_transposed=False, **base)
+    on = _run(t_on, 4, 2, free_port)
+    off = _run(t_off, 4, 2, free_port + 1)
+    _close(on, off, rtol=2e-2, atol=1e-4)          # bf16 working copies: GEMM order may differ by one rounding
+    for i, (src, dst) in enumerate(((t_on, t_off), (t_off, t_on))):
+        d = str(tmp_path / f"ck{i}")
+        # 2 of the 4 steps in the source layout, checkpointed sharded; the other 2 resumed in the other layout
+        _run(src, 4, 2, free_port + 2 + 2 * i, ckpt_dir=d, ckpt_format="sharded", stop_after=2)
+        resumed = _run(dst, 4, 2, free_port + 3 + 2 * i, resume=d)
+        _close(resumed, on, rtol=2e-2, atol=1e-4)

@@ -54,3 +54,64 @@ def test_probe_detects_sharing_without_reservation():
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     rep = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("JSON")][0][4:])["report"]
     assert rep["pool_streams_on_compute_queue"] > 0, rep
+
+
+ROLE_SCRIPT = r"""
+import json, os, sys, time, ctypes, torch
+import torch.distributed as dist
+import dllm
+from dllm import _native
+from dllm.utils import streams
+from dllm.parallel.mesh import Mesh, init_distributed
+backend = sys.argv[1]
+os.environ["LOCAL_RANK"] = "0"
+init_distributed("nccl", 0, 1, "127.0.0.1", 29000 + os.getpid() % 1000)   # reserves the compute queue first
+dev = torch.device("cuda", 0)
+mesh = Mesh.build(1, 1, force=True, comm_backend=backend, device=dev)
+rs = dict(mesh.role_streams)
+rep = streams.role_queue_report(dev, rs)
+out = {"role_streams": {k: (v is not None) for k, v in rs.items()}, "report": rep}
+if backend == "torch":
+    # the identified stream IS the process group's: a collective issued on dp_ag queues behind a spin on that stream,
+    # and not behind a spin on dp_rs's stream (a different queue)
+    sink = torch.zeros(1024, device=dev)
+    def delay(spin_stream):
+        torch.cuda.synchronize()
+        rc = _native.lib().dllm_occupy(1, 64, ctypes.c_float(60000.0), ctypes.c_void_p(sink.data_ptr()),
+                                       ctypes.c_void_p(spin_stream))
+        assert rc == 0, rc
+        t = torch.ones(256, device=dev)
+        t0 = time.perf_counter()
+        w = dist.all_reduce(t, group=mesh.groups["dp_ag"], async_op=True)
+        while not w.is_completed():
+            time.sleep(0.0005)
+        dt = time.perf_counter() - t0
+        torch.cuda.synchronize()
+        return dt * 1e3
+    out["delay_own_ms"] = delay(rs["dp_ag"])
+    out["delay_other_ms"] = delay(rs["dp_rs"])
+mesh.destroy()
+print("JSON" + json.dumps(out))
+dist.destroy_process_group()
+"""
+
+
+@pytest.mark.parametrize("backend", ["torch", "native"])
+def test_role_communicators_on_distinct_queues(backend):
+    """the FSDP gather (dp_ag) and reduce-scatter (dp_rs) communicators' streams run on different
+    hardware queues, and no role communicator shares the compute stream's -- measured on the real process-group streams
+    (torch: identified in torch's stream pool and steered at mesh build; native: our own streams), at HIP's default 4
+    queues.  For torch the identification is checked behaviourally: a dp_ag collective waits for a 60 ms spin on the
+    identified stream but not for one on dp_rs's."""
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    env.pop("GPU_MAX_HW_QUEUES", None)
+    r = subprocess.run([sys.executable, "-c", ROLE_SCRIPT, backend], capture_output=True, text=True, timeout=300,
+                       cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("JSON")][0][4:])
+    assert all(out["role_streams"].values()), out
+    assert out["report"]["role_queue_conflicts"] == [], out
+    assert ["dp_ag", "dp_rs"] not in out["report"]["queue_sharing_pairs"], out
+    if backend == "torch":
+        assert out["delay_own_ms"] > 40.0, out
+        assert out["delay_other_ms"] < 30.0, out
