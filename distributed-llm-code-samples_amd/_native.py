@@ -47,8 +47,6 @@ _SIGS = {
     "dllm_split_master": (c_int, [c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p]),
     "dllm_adam_split_step": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_long, c_float,
                                      c_float, c_float, c_float, c_float, c_int, c_float, c_void_p]),
-    "dllm_adam_split_step_blocks": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_long, c_float,
-                                            c_float, c_float, c_float, c_float, c_int, c_float, c_int, c_void_p]),
     "dllm_cast": (c_int, [c_void_p, c_int, c_void_p, c_int, c_long, c_void_p]),
     "dllm_split3": (c_int, [c_void_p, c_long, c_long, c_long, c_void_p, c_int, c_int, c_void_p]),
     "dllm_occupy": (c_int, [c_int, c_int, c_float, c_void_p, c_void_p]),

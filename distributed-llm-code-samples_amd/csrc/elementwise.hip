@@ -418,18 +418,6 @@ int dllm_adam_split_step(void* lo, void* hi, const void* grad, int grad_dtype, f
   return (int)hipGetLastError();
 }
 
-// the same update as dllm_adam_split_step, bitwise, on at most max_blocks workgroups (side-stream AdamW next to GEMMs)
-int dllm_adam_split_step_blocks(void* lo, void* hi, const void* grad, int grad_dtype, float* m, float* v, long n,
-                                float lr, float b1, float b2, float eps, float wd, int step, float gscale, int max_blocks,
-                                void* stream) {
-  if (n % 4 || step < 1 || max_blocks <= 0 || ((uintptr_t)lo | (uintptr_t)hi) % 8) return -1;
-  const float bc1 = 1.f - powf(b1, (float)step), bc2 = 1.f - powf(b2, (float)step);
-  const int g = std::min(grid_for(n / 4), max_blocks);
-  hipLaunchKernelGGL(adam_split_kernel, dim3(g), dim3(256), 0, (hipStream_t)stream, (uint16_t*)lo, (uint16_t*)hi, grad,
-                     grad_dtype, m, v, n, lr, b1, b2, eps, wd, bc1, bc2, gscale);
-  return (int)hipGetLastError();
-}
-
 // mode 0: out_f32 = join(hi, lo);  mode 1: (hi, lo) = split(in_f32)
 int dllm_split_master(void* hi, void* lo, void* f32, long n, int mode, void* stream) {
   if (n <= 0) return 0;

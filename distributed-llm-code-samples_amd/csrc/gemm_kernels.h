@@ -1327,10 +1327,10 @@ __device__ __forceinline__ void gemm_8ph_body(const GemmArgs& p, const int which
   DLLM_BARRIER();
 #if DLLM_BPRE
     // Balanced fragment reads (round 5).  The fragment-read segment of phase P overlaps the SIMD partner's MFMA
-    // segment; the old order read A0 + B0 (12 of the K-tile's 24 fragments) before q0 and nothing before q3, so the
-    // q0 segment outlasted the partner's 16 MFMAs.  Here each K-tile's B-half 0 is read one phase early, in the
-    // previous quadrant q3 (into whichever B register set q2 has finished with: fb0 / fb1 alternate per K-tile), so
-    // the segments carry 8 / 4 / 8 / 4 fragments.  The MFMA sequence is unchanged (bitwise the same results).
+    // segment; the round-4 order read A0 + B0 (12 of the K-tile's 24 fragments) before q0 and nothing before q3.
+    // Here each K-tile's B-half 0 is read one phase early, in the previous quadrant q3 (into whichever B register set
+    // q2 has finished with: fb0 / fb1 alternate per K-tile), so the segments carry 8 / 4 / 8 / 4 fragments: +0.2 to
+    // +3.1 % per FFN GEMM (profiles/r5/gemm_bpre_ab_r5.txt).  The MFMA sequence is unchanged (bitwise the same results).
     // That read needs the next buffer's B0 retired one phase earlier: vmcnt(8) at P2 / P6 (after the stage, 4
     // half-tiles left in flight) retires the B0 staged at P6 / P2 before, read at P3 / P7.
 #define DLLM_PHASE_END8()                                           \

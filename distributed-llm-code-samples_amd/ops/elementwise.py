@@ -158,22 +158,14 @@ def sgd_split_step_(lo: torch.Tensor, hi: torch.Tensor, grad: torch.Tensor, lr: 
 
 def adam_split_step_(lo: torch.Tensor, hi: torch.Tensor, grad: torch.Tensor, m: torch.Tensor, v: torch.Tensor,
                      step: int, lr: float, b1: float = 0.9, b2: float = 0.95, eps: float = 1e-8, wd: float = 0.0,
-                     grad_scale: float = 1.0, max_blocks: int = 0) -> None:
-    """``adam_step_`` on a split master (``ops/master.py``); the moments ``m`` / ``v`` stay fp32.  ``max_blocks > 0``:
-    the same update (bitwise) on at most that many workgroups -- a side-stream optimizer next to running GEMMs."""
+                     grad_scale: float = 1.0) -> None:
+    """``adam_step_`` on a split master (``ops/master.py``); the moments ``m`` / ``v`` stay fp32."""
     if lo.dtype != torch.int16 or hi.dtype != torch.bfloat16 or lo.numel() != hi.numel():
         raise TypeError("adam_split_step_ takes an int16 residual plane and its bf16 working copy")
     if lo.device.type == "cuda":
         n = lo.numel()
         if n % 4:
             raise ValueError("adam_split_step_ on GPU needs numel % 4 == 0")
-        if max_blocks > 0:
-            rc = _native.lib().dllm_adam_split_step_blocks(
-                lo.data_ptr(), hi.data_ptr(), grad.data_ptr(), _grad_code(grad), m.data_ptr(), v.data_ptr(), n,
-                float(lr), float(b1), float(b2), float(eps), float(wd), int(step), float(grad_scale), int(max_blocks),
-                _native.stream_ptr(lo.device))
-            _native.check(rc, "dllm_adam_split_step_blocks")
-            return
         rc = _native.lib().dllm_adam_split_step(lo.data_ptr(), hi.data_ptr(), grad.data_ptr(), _grad_code(grad),
                                                 m.data_ptr(), v.data_ptr(), n, float(lr), float(b1), float(b2),
                                                 float(eps), float(wd), int(step), float(grad_scale),

@@ -251,16 +251,14 @@ class FFNTrainer:
         no_coll = not (self.ddp or self.fsdp or self.zero)
         # side-stream optimizer: wgrad GEMMs store the gradient, a low-occupancy SGD kernel on its own
         # stream updates the weight while the next GEMMs run; the forward waits per weight
-        # SGD: fp32 master (dllm_sgd_step_stream); AdamW (round 5): split master, the 24 B/param of
-        # master + moments streamed by adam_split_kernel on at most side_optimizer workgroups
-        self.side_opt = (no_coll and cfg.side_optimizer > 0 and dev.type == "cuda" and
-                         (cfg.optimizer == "sgd" or (cfg.optimizer == "adam" and cfg.master == "split"
-                                                     and self.cd == torch.bfloat16)))
+        # (SGD only: a side-stream AdamW on the split master was measured 63 % slower on config 5 and removed, round 5,
+        # profiles/r5/adamw_fused_vs_side_r5.txt)
+        self.side_opt = (no_coll and cfg.side_optimizer > 0 and cfg.optimizer == "sgd" and dev.type == "cuda")
         # Split master (bf16 SGD): the fp32 master is the bf16 working copy (hi) plus an int16 residual plane (lo),
         # bitwise the same fp32 values (ops/master.py).  4 B/param of weight state instead of 6 B, and every update
         # (fused wgrad epilogue or flat kernel) reads 4 B and writes 4 B per parameter instead of 4 B + 6 B.
         nmaster = self.shard_total if self.zero else self.total
-        self.split = cfg.master == "split" and self.cd == torch.bfloat16 and (not self.side_opt or cfg.optimizer == "adam")
+        self.split = cfg.master == "split" and self.cd == torch.bfloat16 and not self.side_opt
         if cfg.master not in ("split", "fp32"):
             raise ValueError(f"unknown master format {cfg.master!r}")
         self._master = None if self.split else torch.zeros(nmaster, dtype=torch.float32, device=dev)
@@ -801,15 +799,9 @@ class FFNTrainer:
             st = self.opt_stream_side
             st.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(st):
-                if self.split:   # AdamW on the split master (the bf16 working copy is its high half)
-                    c = self.cfg
-                    adam_split_step_(self.master_lo[s_:e_], self.copy[s_:e_], self.grads[s_:e_], self.adam_m[s_:e_],
-                                     self.adam_v[s_:e_], self.step_count, c.lr, c.adam_b1, c.adam_b2, c.adam_eps,
-                                     c.weight_decay, max_blocks=c.side_optimizer)
-                else:
-                    copy = None if self.shared_copy else self.copy[s_:e_]
-                    sgd_step_(self._master[s_:e_], self.grads[s_:e_], self.cfg.lr, copy=copy,
-                              max_blocks=self.cfg.side_optimizer)
+                copy = None if self.shared_copy else self.copy[s_:e_]
+                sgd_step_(self._master[s_:e_], self.grads[s_:e_], self.cfg.lr, copy=copy,
+                          max_blocks=self.cfg.side_optimizer)
                 ev = torch.cuda.Event()
                 ev.record(st)
             self.opt_done[(l, name)] = ev
