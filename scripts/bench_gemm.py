@@ -101,7 +101,8 @@ def main():
     if a.cases:
         cases = {k: v for k, v in cases.items() if any(c in k for c in a.cases.split(","))}
     for name, (mine, ref) in cases.items():
-        times = {v: [] for v in variants}
+        run_variants = variants
+        times = {v: [] for v in run_variants}
         if libs:   # bitwise check of every build against the first, from the same initial state
             init = [t.clone() for t in state]
             got = {}
@@ -122,7 +123,7 @@ def main():
                 print(f"  bitwise {v} == {variants[0]}: {same}", flush=True)
         tr = []
         for _ in range(a.rounds):  # interleaved rounds in one process (guide §5.4 rule 24)
-            for v in variants:
+            for v in run_variants:
                 if v in libs:
                     _native._LIB = libs[v]
                     set_bf16_variant("8phase_stagger")
@@ -146,7 +147,7 @@ def main():
             r = statistics.median(tr)
             row = {"torch_ms": r, "torch_tflops": flops / r / 1e9}
             msg += f" torch {flops / r / 1e9:7.1f} TF |"
-        for v in variants:
+        for v in run_variants:
             m = statistics.median(times[v])
             row[v + "_ms"], row[v + "_tflops"] = m, flops / m / 1e9
             msg += f" {v} {flops / m / 1e9:7.1f} TF"
