@@ -23,7 +23,7 @@ _ERR: str | None = None
 c_int, c_long, c_float, c_void_p, c_ull = ctypes.c_int, ctypes.c_long, ctypes.c_float, ctypes.c_void_p, ctypes.c_ulonglong
 
 # bumped with every signature or stream-semantics change below (csrc/elementwise.hip dllm_abi_version): a stale library fails loudly
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 _SIGS = {
     "dllm_gemm": (c_int, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_long, c_void_p, c_long, c_void_p, c_long,
@@ -49,6 +49,7 @@ _SIGS = {
                                      c_float, c_float, c_float, c_float, c_int, c_float, c_void_p]),
     "dllm_cast": (c_int, [c_void_p, c_int, c_void_p, c_int, c_long, c_void_p]),
     "dllm_split3": (c_int, [c_void_p, c_long, c_long, c_long, c_void_p, c_int, c_int, c_void_p]),
+    "dllm_transpose_bf16": (c_int, [c_void_p, c_long, c_void_p, c_long, c_long, c_long, c_void_p]),
     "dllm_occupy": (c_int, [c_int, c_int, c_float, c_void_p, c_void_p]),
     "dllm_abi_version": (c_int, []),
 }

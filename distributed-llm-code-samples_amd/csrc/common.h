@@ -31,8 +31,16 @@ enum Layout : int { L_NT = 0, L_NN = 1, L_TN = 2 };
 //   EPI_SGDS  : EPI_SGD on a split master (below): C = the 16-bit residual plane, aux_out = the bf16 working copy
 //               (required); reads 4 B and writes 4 B per parameter instead of reading 4 B and writing 6 B
 //   EPI_ADAMS : EPI_ADAM on a split master (the moments stay fp32)
+// Transposed outputs (round 5, the NN weight-gradient layout; 8-phase 256x256 kernels only):
+//   EPI_SGDS_T : EPI_SGDS of Cᵀ: the GEMM's [M, N] result updates a split master stored [N, M] (C / aux_out ld'd
+//                as N rows of M), e.g. dW1ᵀ = xᵀ·da into W1 [F, D]; the MFMA operands are swapped so each lane
+//                holds 4 consecutive M (paired 16-B accesses as EPI_SGDS)
+//   EPI_STORE_T : EPI_STORE of Cᵀ (beta = 0), same operand order
+//   EPI_STORE_DT: EPI_STORE (beta = 0, bf16) plus a transposed copy Cᵀ [N, M] into aux_out (ldaux), e.g. a layer's
+//                 output y and its yᵀ for the next layer's NN weight gradient
 enum Epi : int { EPI_STORE = 0, EPI_ACT = 1, EPI_DACT = 2, EPI_GLU = 3, EPI_DGLU = 4, EPI_SGD = 5, EPI_ADAM = 6,
-                 EPI_SGDS = 7, EPI_ADAMS = 8 };
+                 EPI_SGDS = 7, EPI_ADAMS = 8, EPI_SGDS_T = 9, EPI_STORE_T = 10, EPI_STORE_DT = 11 };
+__host__ __device__ constexpr bool epi_tout(int e) { return e == EPI_SGDS_T || e == EPI_STORE_T; }
 enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_SILU = 2, ACT_GELU = 3 };
 
 __device__ __forceinline__ float bf2f(uint16_t v) {

@@ -346,6 +346,35 @@ __global__ void stamp_kernel(unsigned long long* out, long ticks) {
   }
 }
 
+// bf16 transpose dst[C][R] = src[R][C] through LDS, 64x64 tiles, 256 threads: 16-B row-chunk loads, the tile kept
+// as 66-element LDS rows (a column gather then spreads over 32 banks), 8-row gathers packed into 16-B stores.  The
+// NN weight-gradient layout's transposed copies of the step's input x (layer 0) and dL/dy (top layer): every other
+// layer's copy comes out of the producing GEMM's epilogue (EPI_STORE_DT).
+__global__ __launch_bounds__(256) void transpose_bf16_kernel(const uint16_t* __restrict__ src, long lds,
+                                                             uint16_t* __restrict__ dst, long ldd) {
+  __shared__ uint32_t sh[64 * 33];
+  const int t = threadIdx.x;
+  const long r0 = (long)blockIdx.y * 64, c0 = (long)blockIdx.x * 64;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int row = t / 8 + 32 * k, ch = t % 8;
+    const uint4 v = *(const uint4*)(src + (r0 + row) * lds + c0 + 8 * ch);
+    uint32_t* w = sh + row * 33 + 4 * ch;
+    w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+  }
+  __syncthreads();
+  const uint16_t* h = (const uint16_t*)sh;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int c = t / 8 + 32 * k, rc = t % 8;
+    uint32_t q[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      q[j] = (uint32_t)h[(8 * rc + 2 * j) * 66 + c] | ((uint32_t)h[(8 * rc + 2 * j + 1) * 66 + c] << 16);
+    *(uint4*)(dst + (c0 + c) * ldd + r0 + 8 * rc) = make_uint4(q[0], q[1], q[2], q[3]);
+  }
+}
+
 static inline int grid_for(long n4) {
   long g = (n4 + 255) / 256;
   if (g > 2048) g = 2048;
@@ -463,6 +492,16 @@ int dllm_split3(const float* src, long lds, long R, long C, void* dst, int role,
   return (int)hipGetLastError();
 }
 
+// dst [C, R] = src [R, C]ᵀ, bf16; R, C multiples of 64, 16-B aligned bases and row strides
+int dllm_transpose_bf16(const void* src, long lds, void* dst, long ldd, long R, long C, void* stream) {
+  if (R <= 0 || C <= 0 || R % 64 || C % 64 || lds % 8 || ldd % 8 || lds < C || ldd < R || (uintptr_t)src % 16 ||
+      (uintptr_t)dst % 16 || R / 64 > 65535)
+    return -1;
+  hipLaunchKernelGGL(transpose_bf16_kernel, dim3(C / 64, R / 64), dim3(256), 0, (hipStream_t)stream,
+                     (const uint16_t*)src, lds, (uint16_t*)dst, ldd);
+  return (int)hipGetLastError();
+}
+
 int dllm_occupy(int blocks, int threads, float us, float* sink, void* stream) {
   if (blocks <= 0 || threads <= 0 || threads > 1024 || us < 0.f || us > 1e5f) return -1;
   hipLaunchKernelGGL(occupy_kernel, dim3(blocks), dim3(threads), 0, (hipStream_t)stream, (long)(us * 100.f), sink);
@@ -524,6 +563,6 @@ int dllm_queue_reserve(void* base, int candidates, int spin_us) {
   return err ? err : nblock;
 }
 
-int dllm_abi_version() { return 12; }
+int dllm_abi_version() { return 13; }
 
 }  // extern "C"

@@ -61,8 +61,8 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
   const bool aligned_ptr = ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && ((uintptr_t)C % 16 == 0) &&
                            ((uintptr_t)aux % 16 == 0) && ((uintptr_t)aux_out % 16 == 0) &&
                            ((uintptr_t)opt_m % 16 == 0) && ((uintptr_t)opt_v % 16 == 0);
-  const bool opt_epi = (epi == EPI_SGD || epi == EPI_ADAM || epi == EPI_SGDS || epi == EPI_ADAMS);
-  const bool split_epi = (epi == EPI_SGDS || epi == EPI_ADAMS);
+  const bool opt_epi = (epi == EPI_SGD || epi == EPI_ADAM || epi == EPI_SGDS || epi == EPI_ADAMS || epi == EPI_SGDS_T);
+  const bool split_epi = (epi == EPI_SGDS || epi == EPI_ADAMS || epi == EPI_SGDS_T);
   if (opt_epi && layout == L_NT) return -1;
   if ((epi == EPI_SGD || epi == EPI_ADAM) && out_dtype != DT_F32) return -1;
   // split master: C = the 16-bit residual plane, aux_out = the bf16 working copy (paired 16-B rows: ld % 8 == 0)
@@ -88,7 +88,22 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
     if (force_path == 3 && path != 3) return -1;
     path = force_path;
   }
-  if (opt_epi && layout == L_NN && path != 3) return -1;  // NN fused optimizers: 224-row tiles only
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e;
+  // The NN weight-gradient layout (transposed outputs, transposed copies, NN fused SGD on 256-row tiles):
+  // 8-phase 256x256 persistent kernels only (gemm_kernels.h dispatch_x)
+  const bool xepi = epi == EPI_SGDS_T || epi == EPI_STORE_T || epi == EPI_STORE_DT;
+  if (xepi || (epi == EPI_SGDS && layout == L_NN && path == 0)) {
+    if (path != 0 || K % (2 * BT_K) != 0 || ksplit > 1 || mask != nullptr || beta != 0.f || ldc % 8 != 0 ||
+        (a.variant != 0 && a.variant != 3))
+      return -1;
+    if (epi == EPI_STORE_DT && (aux_out == nullptr || out_dtype != DT_BF16 || ldaux % 8 != 0 || layout == L_TN))
+      return -1;
+    if (epi != EPI_STORE_DT && layout != L_NN) return -1;
+    e = layout == L_NN ? dispatch_nn_x(epi, a, out_dtype, s) : dispatch_nt_x(epi, a, out_dtype, s);
+    return (int)e;
+  }
+  if (opt_epi && layout == L_NN && path != 3) return -1;  // NN fused optimizers otherwise: 224-row tiles only
   if (path == 2 && epi == EPI_GLU && aux_out == nullptr) return -1;
   if (ksplit > 1) {
     // split-K only on the bf16 8-phase path (each slice an even number of 64-deep K-tiles); a request
@@ -106,8 +121,6 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
       return -2;
     a.mask = mask;
   }
-  hipStream_t s = (hipStream_t)stream;
-  hipError_t e;
   if (opt_epi) {
     e = (layout == L_NN && path == 3) ? dispatch_nn_opt(epi, a, s) : dispatch_tn_opt(path, epi, a, in_dtype, s);
     return (int)e;

@@ -292,6 +292,32 @@ __device__ __forceinline__ void unpair_bf16(uint4 v, f32x4_t& a, f32x4_t& b) {
   b = Raw4<uint16_t>::cvt(uint2{u.z, u.w});
 }
 
+// 4x4 transpose across the lanes of a quad (lanes 4j .. 4j+3, element e = column): lane 4j + i returns column i,
+// i.e. element e = the input element i of lane 4j + e.  Two xor exchanges (DPP quad_perm, no LDS): off-diagonal 2x2
+// blocks between lanes i, i^2, then single elements between lanes i, i^1.  EXEC must be full (the epilogues are).
+template <int CTRL> __device__ __forceinline__ float dpp_f(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ f32x4_t quad_transpose(f32x4_t v, int lane) {
+  constexpr int XOR2 = 2 | (3 << 2) | (0 << 4) | (1 << 6);  // quad_perm [2, 3, 0, 1]
+  constexpr int XOR1 = 1 | (0 << 2) | (3 << 4) | (2 << 6);  // quad_perm [1, 0, 3, 2]
+  const bool hi = lane & 2, lo = lane & 1;
+  const float d0 = dpp_f<XOR2>(v[0]), d1 = dpp_f<XOR2>(v[1]), d2 = dpp_f<XOR2>(v[2]), d3 = dpp_f<XOR2>(v[3]);
+  const f32x4_t t{hi ? d2 : v[0], hi ? d3 : v[1], hi ? v[2] : d0, hi ? v[3] : d1};
+  const float u0 = dpp_f<XOR1>(t[0]), u1 = dpp_f<XOR1>(t[1]), u2 = dpp_f<XOR1>(t[2]), u3 = dpp_f<XOR1>(t[3]);
+  return f32x4_t{lo ? u1 : t[0], lo ? t[1] : u0, lo ? u3 : t[2], lo ? t[3] : u2};
+}
+// Pairs two quad-transposed fragments 16 rows apart (x: rows 4j..4j+3 of the first, y: of the second, packed bf16)
+// across lanes 4 apart (DPP row_shl:4 / row_shr:4 inside each 16-lane row): lanes with j = (lane>>2)&3 even return the
+// first fragment's rows 4j .. 4j+7, odd ones the second fragment's rows 4(j-1) .. 4(j-1)+7 -- 8 consecutive rows each.
+__device__ __forceinline__ uint4 tpair_bf16(uint2 x, uint2 y, int lane) {
+  const uint32_t x0 = __builtin_amdgcn_update_dpp(0, (int)x.x, 0x104, 0xf, 0xf, false);  // row_shl:4: lane + 4
+  const uint32_t x1 = __builtin_amdgcn_update_dpp(0, (int)x.y, 0x104, 0xf, 0xf, false);
+  const uint32_t y0 = __builtin_amdgcn_update_dpp(0, (int)y.x, 0x114, 0xf, 0xf, false);  // row_shr:4: lane - 4
+  const uint32_t y1 = __builtin_amdgcn_update_dpp(0, (int)y.y, 0x114, 0xf, 0xf, false);
+  return (lane & 4) ? uint4{y0, y1, y.x, y.y} : uint4{x.x, x.y, x0, x1};
+}
+
 // acc[QM][QN][mt][nt]: lane holds C[m0 + QM*128 + wr*64 + mt*16 + (lane&15)][n0 + QN*QNS + wc*32 + nt*16 + 4*(lane>>4) + 0..3]
 // row group rg = QM*8 + QN*4 + mt (16 per wave), 2 column groups (nt) each.  QNS = quadrant width: 128 for the
 // 256x256 tile (8 waves, wc 0..3), 64 for the 256x128 tile of gemm_bf16_pp (4 waves, wc 0..1).
@@ -301,6 +327,7 @@ template <int EPI, typename OutT, int ACT, int QNS = 128, int BM = 256>
 __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2][2][4][2], int m0, int n0,
                                              int wr, int wc, int lane, void* Cp) {
   static_assert(BM == 256 || (QNS == 128 && EPI != EPI_GLU && EPI != EPI_DGLU), "224-row tiles: no gated epilogues");
+  static_assert(!(epi_tout(EPI) || EPI == EPI_STORE_DT) || (BM == 256 && QNS == 128), "transposed outputs: 256x256");
   constexpr int NWC = QNS / 32;       // waves per tile row
   constexpr int TW = 2 * QNS;         // tile width
   constexpr int MASK_WAVES = 2 * NWC; // waves per tile: the ReLU mask holds 16 B per lane and wave
@@ -311,8 +338,10 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
   constexpr int WR = BF ? 4 : 8;  // VGPRs per row group and loaded operand
   // (the beta != 0 store path is off the FFN hot path: small batches keep the persistent kernel's
   // in-loop epilogue within the register budget)
-  constexpr int COST = EPI == EPI_DACT ? WR : EPI == EPI_DGLU ? 8 * (BF ? 2 : 4) : EPI == EPI_STORE ? 4 * WR
-                     : EPI == EPI_SGD || EPI == EPI_SGDS ? 8 : EPI == EPI_ADAM || EPI == EPI_ADAMS ? 24 : 0;
+  constexpr int COST = EPI == EPI_DACT ? WR : EPI == EPI_DGLU ? 8 * (BF ? 2 : 4)
+                     : EPI == EPI_STORE || EPI == EPI_STORE_T || EPI == EPI_STORE_DT ? 4 * WR
+                     : EPI == EPI_SGD || EPI == EPI_SGDS || EPI == EPI_SGDS_T ? 8
+                     : EPI == EPI_ADAM || EPI == EPI_ADAMS ? 24 : 0;
   constexpr int RB = epi_batch(COST);
   const int pc = pair_col(lane);
 #define DLLM_M(rg) (m0 + ((rg) >> 3) * 128 + wr * ((BM != 256 && ((rg) >> 3)) ? 48 : 64) + ((rg) & 3) * 16 + (lane & 15))
@@ -320,6 +349,23 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
 #define DLLM_NB(rg) (n0 + (((rg) >> 2) & 1) * QNS + wc * 32)
 #define DLLM_N(rg, nt) (DLLM_NB(rg) + (nt) * 16 + 4 * (lane >> 4))
 #define DLLM_ACC(rg, nt) acc[(rg) >> 3][((rg) >> 2) & 1][(rg) & 3][nt]
+  // Transposed outputs (epi_tout: MFMA operands swapped in the main loop): lane holds
+  // C[m0 + QM*128 + wr*64 + mt*16 + 4*(lane>>4) + e][n0 + QN*QNS + wc*32 + nt*16 + (lane&15)], written to Cᵀ [N][M].
+  // Row group rg = (QM, QN, nt, p) is output row n = ...(lane&15) and pairs fragments mt = 2p, 2p+1 (32 consecutive
+  // m), exactly as the normal layout pairs nt = 0, 1 -- so the paired 16-B accesses below serve both.
+  constexpr bool TRO = epi_tout(EPI);
+  auto row_of = [&](int rg) -> int {
+    if constexpr (TRO) return n0 + ((rg >> 2) & 1) * QNS + wc * 32 + ((rg >> 1) & 1) * 16 + (lane & 15);
+    else return DLLM_M(rg);
+  };
+  auto colb_of = [&](int rg) -> int {
+    if constexpr (TRO) return m0 + (rg >> 3) * 128 + wr * 64 + (rg & 1) * 32;
+    else return DLLM_NB(rg);
+  };
+  auto acc_of = [&](int rg, int h) -> f32x4_t {
+    if constexpr (TRO) return acc[rg >> 3][(rg >> 2) & 1][2 * (rg & 1) + h][(rg >> 1) & 1];
+    else return DLLM_ACC(rg, h);
+  };
   // store the row group's two fragments (already epilogue-transformed) to a [*, ld] OutT matrix
   auto store_rg = [&](void* base, long ld, int m, int nb, f32x4_t a, f32x4_t b) {
     if constexpr (BF) {
@@ -342,7 +388,33 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
     if constexpr (BF) unpair_bf16(src[0], a, b);
     else { a = src[0]; b = src[1]; }
   };
-  if constexpr (EPI == EPI_STORE) {
+  if constexpr (EPI == EPI_STORE_T) {
+#pragma unroll
+    for (int rg = 0; rg < 16; ++rg)
+      store_rg(Cp, p.ldc, row_of(rg), colb_of(rg), acc_of(rg, 0) * p.alpha, acc_of(rg, 1) * p.alpha);
+  } else if constexpr (EPI == EPI_STORE_DT) {
+    // C as EPI_STORE, then Cᵀ [N][M] into aux_out: per fragment a quad transpose gives lane 4j + i the 4 rows
+    // m = mb + 4j .. 4j+3 of column n = nb + nt*16 + 4*(lane>>4) + i -> one 8-B store into row n of Cᵀ
+    static_assert(BF, "transposed copy: bf16 output");
+    // C as EPI_STORE; then Cᵀ [N][M] into aux_out.  Per fragment a quad transpose gives lane 4j + i the 4 rows
+    // m = 4j .. 4j+3 (of the fragment's 16) of column n = nb + nt*16 + 4*(lane>>4) + i; the fragments of row groups
+    // rg, rg+1 (rows 16 apart) are then paired across lanes 4 apart (tpair_bf16), so each lane stores 8 consecutive
+    // m -- one 16-B store per lane covering 16 rows of Cᵀ x 64 contiguous bytes, the shape of the paired row store
+    const int j4 = (lane >> 2) & 3;
+    const int mq = 16 * (j4 & 1) + 4 * (j4 & 2) - (lane & 15);  // DLLM_M(rg) + mq = the lane's first row
+    const int nq = 4 * (lane >> 4) + (lane & 3);
+#pragma unroll
+    for (int rg = 0; rg < 16; rg += 2) {
+      const f32x4_t a00 = DLLM_ACC(rg, 0) * p.alpha, a01 = DLLM_ACC(rg, 1) * p.alpha;
+      const f32x4_t a10 = DLLM_ACC(rg + 1, 0) * p.alpha, a11 = DLLM_ACC(rg + 1, 1) * p.alpha;
+      store_rg(Cp, p.ldc, DLLM_M(rg), DLLM_NB(rg), a00, a01);
+      store_rg(Cp, p.ldc, DLLM_M(rg + 1), DLLM_NB(rg + 1), a10, a11);
+      uint16_t* tb = (uint16_t*)p.aux_out + (long)(DLLM_NB(rg) + nq) * p.ldaux + DLLM_M(rg) + mq;
+      *(uint4*)tb = tpair_bf16(pk_bf16(quad_transpose(a00, lane)), pk_bf16(quad_transpose(a10, lane)), lane);
+      *(uint4*)(tb + 16 * p.ldaux) =
+          tpair_bf16(pk_bf16(quad_transpose(a01, lane)), pk_bf16(quad_transpose(a11, lane)), lane);
+    }
+  } else if constexpr (EPI == EPI_STORE) {
     if (p.beta == 0.f) {
 #pragma unroll
       for (int rg = 0; rg < 16; ++rg)
@@ -565,18 +637,19 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
             st_pair_bf16(p.aux_out, (long)DLLM_M(b0 + r) * p.ldaux + DLLM_NB(b0 + r) + pc, W[r][0], W[r][1]);
       }
     }
-  } else if constexpr (EPI == EPI_SGDS) {
+  } else if constexpr (EPI == EPI_SGDS || EPI == EPI_SGDS_T) {
     // split master: hi plane = the bf16 working copy (aux_out), lo plane = the 16-bit residual (Cp), both in the
     // paired 16-B layout: per row group one 16-B load and one 16-B store per plane (4 B read + 4 B written per
-    // parameter; the fp32 master form moves 4 B + 6 B in 5 accesses)
+    // parameter; the fp32 master form moves 4 B + 6 B in 5 accesses).  EPI_SGDS_T: the same on the transposed map
+    // (row_of / colb_of / acc_of)
 #pragma unroll
     for (int b0 = 0; b0 < 16; b0 += RB) {
       uint4 H[RB], Lw[RB];
 #pragma unroll
       for (int r = 0; r < RB; ++r) {
         if (!DLLM_OK(b0 + r)) continue;
-        H[r] = *(const uint4*)((const uint16_t*)p.aux_out + (long)DLLM_M(b0 + r) * p.ldaux + DLLM_NB(b0 + r) + pc);
-        Lw[r] = *(const uint4*)((const uint16_t*)Cp + (long)DLLM_M(b0 + r) * p.ldc + DLLM_NB(b0 + r) + pc);
+        H[r] = *(const uint4*)((const uint16_t*)p.aux_out + (long)row_of(b0 + r) * p.ldaux + colb_of(b0 + r) + pc);
+        Lw[r] = *(const uint4*)((const uint16_t*)Cp + (long)row_of(b0 + r) * p.ldc + colb_of(b0 + r) + pc);
       }
 #pragma unroll
       for (int r = 0; r < RB; ++r) {
@@ -584,7 +657,7 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
         // after the exchange: words 0-1 hold the nt = 0 fragment's 4 columns, words 2-3 the nt = 1 fragment's
         const uint4 h = pair_swap(uint2{H[r].x, H[r].y}, uint2{H[r].z, H[r].w});
         const uint4 l = pair_swap(uint2{Lw[r].x, Lw[r].y}, uint2{Lw[r].z, Lw[r].w});
-        const f32x4_t g0 = DLLM_ACC(b0 + r, 0), g1 = DLLM_ACC(b0 + r, 1);
+        const f32x4_t g0 = acc_of(b0 + r, 0), g1 = acc_of(b0 + r, 1);
         uint32_t hw[4] = {h.x, h.y, h.z, h.w}, lw[4] = {l.x, l.y, l.z, l.w};
         const float gg[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
 #pragma unroll
@@ -595,9 +668,9 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
           f1 = __fadd_rn(f1, __fmul_rn(-p.lr, __fmul_rn(p.alpha, gg[2 * j + 1])));
           split_part2(f0, f1, hw[j], lw[j]);
         }
-        *(uint4*)((uint16_t*)p.aux_out + (long)DLLM_M(b0 + r) * p.ldaux + DLLM_NB(b0 + r) + pc) =
+        *(uint4*)((uint16_t*)p.aux_out + (long)row_of(b0 + r) * p.ldaux + colb_of(b0 + r) + pc) =
             pair_swap(uint2{hw[0], hw[1]}, uint2{hw[2], hw[3]});
-        *(uint4*)((uint16_t*)Cp + (long)DLLM_M(b0 + r) * p.ldc + DLLM_NB(b0 + r) + pc) =
+        *(uint4*)((uint16_t*)Cp + (long)row_of(b0 + r) * p.ldc + colb_of(b0 + r) + pc) =
             pair_swap(uint2{lw[0], lw[1]}, uint2{lw[2], lw[3]});
       }
     }
@@ -1240,8 +1313,12 @@ __device__ __forceinline__ void gemm_8ph_body(const GemmArgs& p, const int which
 #pragma unroll
       for (int mt = 0; mt < NMT; ++mt)
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
-          c[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[nt][s2], fa[mt][s2], c[mt][nt], 0, 0, 0);
+        for (int nt = 0; nt < 2; ++nt) {
+          if constexpr (epi_tout(EPI))  // transposed output: lane ends with 4 consecutive rows of one column
+            c[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mt][s2], fb[nt][s2], c[mt][nt], 0, 0, 0);
+          else
+            c[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[nt][s2], fa[mt][s2], c[mt][nt], 0, 0, 0);
+        }
 #if DLLM_PRIO_MODE == 0
     __builtin_amdgcn_s_setprio(0);
 #endif
@@ -2051,10 +2128,41 @@ static hipError_t launch_splitk(const GemmArgs& a, int out_dt, float* ws, hipStr
 template <int L, int E, typename OutT, int ACT>
 constexpr bool persistent_kernel() {
   constexpr bool bf = std::is_same<OutT, uint16_t>::value;
+  if constexpr (E == EPI_STORE_DT || E == EPI_STORE_T || E == EPI_SGDS_T) return true;
+  if constexpr (L == L_NN && E == EPI_SGDS) return true;   // the NN weight-gradient layout (dispatch_x)
   // gated (SwiGLU) stacks: the GLU forward / DGLU dgrad with a compile-time activation (round 3)
   if constexpr (L == L_NT) return bf && ((E == EPI_ACT && ACT == ACT_RELU) || E == EPI_STORE || (E == EPI_GLU && ACT >= 0));
   if constexpr (L == L_NN) return bf && ((E == EPI_DACT && ACT == ACT_RELU) || E == EPI_STORE || (E == EPI_DGLU && ACT >= 0));
   return E == EPI_STORE || E == EPI_SGD || E == EPI_SGDS;
+}
+
+// The NN weight-gradient layout's GEMMs (round 5; 8-phase 256x256 tiles, K % 128 == 0, no split-K): NN fused SGD on
+// a split master (dW2 = dyᵀ·a with dyᵀ [D, T] K-contiguous), NN with a transposed output (dW1ᵀ = xᵀ·da into W1
+// [F, D]: EPI_SGDS_T / EPI_STORE_T), and plain stores that also write a transposed copy (EPI_STORE_DT, NT y or NN dx).
+template <int L>
+static hipError_t dispatch_x(int epi, const GemmArgs& a, int out_dt, hipStream_t s) {
+  const int nb = (a.M / BT_M) * (a.N / BT_N);
+  const bool f32 = out_dt == DT_F32;
+  switch (epi) {
+    case EPI_STORE_DT:
+      if (f32) return hipErrorInvalidValue;
+      launch_8ph_act<L, EPI_STORE_DT, uint16_t, -1, 8>(a, nb, s);
+      break;
+    case EPI_STORE_T:
+    case EPI_SGDS_T:
+    case EPI_SGDS:
+      if constexpr (L == L_NN) {
+        if (epi == EPI_SGDS) launch_8ph_act<L, EPI_SGDS, float, -1, 8>(a, nb, s);
+        else if (epi == EPI_SGDS_T) launch_8ph_act<L, EPI_SGDS_T, float, -1, 8>(a, nb, s);
+        else if (f32) launch_8ph_act<L, EPI_STORE_T, float, -1, 8>(a, nb, s);
+        else launch_8ph_act<L, EPI_STORE_T, uint16_t, -1, 8>(a, nb, s);
+        break;
+      } else {
+        return hipErrorInvalidValue;
+      }
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
 }
 
 template <int L, int E, typename OutT, int ACT, int NPH>
@@ -2238,5 +2346,7 @@ hipError_t dispatch_tn_opt(int path, int epi, const GemmArgs& a, int in_dt, hipS
 hipError_t dispatch_tn_pair(int epi, const GemmArgs& a0, const GemmArgs& a1, int out_dt, hipStream_t s);
 hipError_t dispatch_nn_pair(int epi, const GemmArgs& a0, const GemmArgs& a1, int out_dt, hipStream_t s);
 hipError_t dispatch_nn_opt(int epi, const GemmArgs& a, hipStream_t s);
+hipError_t dispatch_nt_x(int epi, const GemmArgs& a, int out_dt, hipStream_t s);
+hipError_t dispatch_nn_x(int epi, const GemmArgs& a, int out_dt, hipStream_t s);
 
 }  // namespace dllm

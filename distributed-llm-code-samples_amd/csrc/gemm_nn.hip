@@ -22,4 +22,7 @@ hipError_t dispatch_nn_opt(int epi, const GemmArgs& a, hipStream_t s) {
   }
 }
 
+// the NN weight-gradient layout's launches (gemm_kernels.h dispatch_x)
+hipError_t dispatch_nn_x(int epi, const GemmArgs& a, int out_dt, hipStream_t s) { return dispatch_x<L_NN>(epi, a, out_dt, s); }
+
 }  // namespace dllm

@@ -8,4 +8,7 @@ hipError_t dispatch_nt(int path, int epi, const GemmArgs& a, int in_dt, int out_
   return dispatch_epi<L_NT>(path, epi, a, in_dt, out_dt, s);
 }
 
+// the NN weight-gradient layout's launches (gemm_kernels.h dispatch_x)
+hipError_t dispatch_nt_x(int epi, const GemmArgs& a, int out_dt, hipStream_t s) { return dispatch_x<L_NT>(epi, a, out_dt, s); }
+
 }  // namespace dllm

@@ -22,6 +22,8 @@ interleaved ``[dg|du]`` that feeds one dgrad and one wgrad GEMM against W13.
 """
 from __future__ import annotations
 
+from typing import NamedTuple
+
 import torch
 
 from ..ops.gemm import gemm, gemm_pair
@@ -94,24 +96,54 @@ def needs_preact(act: str, gated: bool) -> bool:
 
 def layer_fwd(x: torch.Tensor, w1: torch.Tensor, w2: torch.Tensor, act: str, gated: bool,
               a_out: torch.Tensor, h_out: torch.Tensor | None, y_out: torch.Tensor,
-              before_fwd2=None, mask: torch.Tensor | None = None) -> torch.Tensor:
+              before_fwd2=None, mask: torch.Tensor | None = None, y_t: torch.Tensor | None = None) -> torch.Tensor:
     """y = act(x·W1ᵀ)·W2ᵀ  (gated: (act(x·W1ᵀ)⊙x·W3ᵀ)·W2ᵀ with ``w1`` = interleaved W13).
     ``before_fwd2()`` runs between the two GEMMs (e.g. waiting for W2's all-gather).  ``mask`` (ReLU):
-    the first GEMM also writes the activation-gradient bitmask the backward's dgrad reads."""
+    the first GEMM also writes the activation-gradient bitmask the backward's dgrad reads.  ``y_t`` (NN weight-gradient
+    layout): the second GEMM's epilogue also writes yᵀ [D, T], the next layer's dW1 operand."""
     if gated:
         gemm(x, w1, "nt", out=a_out, epi="glu", act=act, aux_out=h_out)
     else:
         gemm(x, w1, "nt", out=a_out, epi="act", act=act, aux_out=h_out, mask=mask)
     if before_fwd2 is not None:
         before_fwd2()
-    gemm(a_out, w2, "nt", out=y_out)
+    gemm(a_out, w2, "nt", out=y_out, aux_t=y_t)
     return y_out
+
+
+class NNWgrad(NamedTuple):
+    """Operands of the NN weight-gradient layout (round 5) for one layer's backward.
+
+    The TN weight gradients ``dW2 = dyᵀ·a`` and ``dW1 = daᵀ·x`` read both operands through transposed LDS fragment
+    reads (twice the read instructions of a K-contiguous operand).  With transposed copies of the two D-sized
+    operands -- ``x_t`` = xᵀ [D, T] (the previous layer's fwd-2 epilogue writes it, ``layer_fwd(y_t=)``) and ``dy_t``
+    = dyᵀ [D, T] (the layer above's dx epilogue writes it, ``dx_t``) -- both run as NN GEMMs with a K-contiguous A:
+    ``dW2 = (dyᵀ)·a`` [D, F] and ``dW1ᵀ = (xᵀ)·da`` [D, F] written transposed into W1 [F, D] (``gemm(out_t=True)``).
+    Same products, same accumulation order: bitwise the TN results (tests/test_gemm_nnwgrad_gpu.py)."""
+    x_t: torch.Tensor
+    dy_t: torch.Tensor
+    dx_t: torch.Tensor | None
+
+
+def wgrad_w2(dy: torch.Tensor, a: torch.Tensor, kw2: dict, nn: NNWgrad | None) -> None:
+    if nn is None:
+        gemm(dy, a, "tn", **kw2)                                      # dW2 = dyᵀ·a        [D, F]
+    else:
+        gemm(nn.dy_t, a, "nn", **kw2)                                 # dW2 = (dyᵀ)·a      [D, F]
+
+
+def wgrad_w1(da: torch.Tensor, x: torch.Tensor, kw1: dict, nn: NNWgrad | None) -> None:
+    if nn is None:
+        gemm(da, x, "tn", **kw1)                                      # dW1 = daᵀ·x        [F, D]
+    else:
+        gemm(nn.x_t, da, "nn", out_t=True, **kw1)                     # dW1ᵀ = (xᵀ)·da     -> W1 [F, D]
 
 
 def layer_bwd(dy: torch.Tensor, x: torch.Tensor, w1: torch.Tensor, w2: torch.Tensor, act: str, gated: bool,
               a: torch.Tensor, h: torch.Tensor | None, gw1, gw2, da_buf: torch.Tensor,
               dx_out: torch.Tensor | None, hooks=None, mask: torch.Tensor | None = None,
-              dx_first: bool = False, pair_wgrads: bool = False) -> torch.Tensor | None:
+              dx_first: bool = False, pair_wgrads: bool = False,
+              nn: NNWgrad | None = None) -> torch.Tensor | None:
     """Backward of one layer; returns dx.
 
     ``gw1``/``gw2`` are either gradient tensors (overwritten) or dicts of ``gemm`` keyword arguments for the
@@ -128,6 +160,8 @@ def layer_bwd(dy: torch.Tensor, x: torch.Tensor, w1: torch.Tensor, w2: torch.Ten
     ``pair_wgrads`` (small tile grids, e.g. the MP / TP8 shard): ``da, dx, (dW2 | dW1)`` -- both weight gradients
     in ONE grouped launch (``ops.gemm.gemm_pair``) that fills the chip with whole tiles instead of two split-K GEMMs
     and their reduction passes; dx still runs before W1's fused update, and a TP all-reduce of dx overlaps the pair.
+
+    ``nn`` (``NNWgrad``): the weight gradients in the NN layout; dx's epilogue also writes dxᵀ into ``nn.dx_t``.
     """
     if gated:
         gemm(dy, w2, "nn", out=da_buf, epi="dglu", act=act, aux=h)    # [dg|du] interleaved [T, 2F]
@@ -150,28 +184,29 @@ def layer_bwd(dy: torch.Tensor, x: torch.Tensor, w1: torch.Tensor, w2: torch.Ten
                 hooks.after_w2()
                 hooks.after_w1()
         return dx
+    dx_t = nn.dx_t if nn is not None else None
     if dx_out is None:
         # no input gradient (layer 0): dW1 first, so W1's gradient collective / update starts while dW2
         # runs and the next forward's first GEMM (which needs W1) is not behind the step's last collective
-        gemm(da_buf, x, "tn", **kw1)                                  # dW1 = daᵀ·x        [F, D]
+        wgrad_w1(da_buf, x, kw1, nn)                                  # dW1 = daᵀ·x        [F, D]
         if hooks is not None:
             hooks.after_w1()
-        gemm(dy, a, "tn", **kw2)                                      # dW2 = dyᵀ·a        [D, F]
+        wgrad_w2(dy, a, kw2, nn)                                      # dW2 = dyᵀ·a        [D, F]
         if hooks is not None:
             hooks.after_w2()
         return None
     if dx_first:
-        dx = gemm(da_buf, w1, "nn", out=dx_out)                       # dx = da·W1         [T, D]
+        dx = gemm(da_buf, w1, "nn", out=dx_out, aux_t=dx_t)           # dx = da·W1         [T, D]
         if hooks is not None:
             hooks.after_dx(dx)
-    gemm(dy, a, "tn", **kw2)                                          # dW2 = dyᵀ·a        [D, F]
+    wgrad_w2(dy, a, kw2, nn)                                          # dW2 = dyᵀ·a        [D, F]
     if hooks is not None:
         hooks.after_w2()
     if not dx_first:
-        dx = gemm(da_buf, w1, "nn", out=dx_out)                       # dx = da·W1         [T, D]
+        dx = gemm(da_buf, w1, "nn", out=dx_out, aux_t=dx_t)           # dx = da·W1         [T, D]
         if hooks is not None:
             hooks.after_dx(dx)
-    gemm(da_buf, x, "tn", **kw1)                                      # dW1 = daᵀ·x        [F, D]
+    wgrad_w1(da_buf, x, kw1, nn)                                      # dW1 = daᵀ·x        [F, D]
     if hooks is not None:
         hooks.after_w1()
     return dx

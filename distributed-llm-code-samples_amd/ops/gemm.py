@@ -22,6 +22,13 @@ followed by an epilogue:
   (required) the bf16 working copy; together they hold the fp32 master, updated exactly as ``"sgd"`` updates it
 * ``"adam_split"``: ``"adam"`` on a split master (fp32 moments ``opt_m``/``opt_v`` in ``C``'s layout)
 
+Transposed outputs (the NN weight-gradient layout, ``ffn.layer_bwd(..., wgrad_nn=...)``; 256x256 8-phase tiles):
+
+* ``out_t=True`` (``"store"``, ``"sgd_split"``, layout ``"nn"``): ``out`` (and ``aux_out``) hold ``Cᵀ`` [N, M] -- e.g.
+  ``dW1ᵀ = xᵀ·da`` written into (or updating) ``W1`` [F, D] while ``xᵀ`` is the K-contiguous A operand
+* ``aux_t=`` (``"store"``, beta 0, bf16, layouts ``"nt"`` / ``"nn"``): also writes ``Cᵀ`` [N, M] into ``aux_t`` --
+  e.g. a layer's output ``y`` and its ``yᵀ``, the next layer's K-contiguous weight-gradient operand
+
 CUDA (HIP) tensors run the hand-written gfx950 kernels of ``csrc/gemm_kernels.h``; CPU tensors run the torch
 reference below (used by the CPU/gloo tests and as the numerics oracle).  There is no silent fallback:
 a GPU tensor with the native library missing raises.
@@ -79,7 +86,7 @@ def _glu_merge(g: torch.Tensor, u: torch.Tensor) -> torch.Tensor:
     return torch.stack([g.reshape(M, F // 16, 16), u.reshape(M, F // 16, 16)], dim=2).reshape(M, 2 * F)
 
 
-def _torch_gemm(a, b, layout, out, epi, act, aux, aux_out, alpha, beta, opt=None):
+def _torch_gemm(a, b, layout, out, epi, act, aux, aux_out, alpha, beta, opt=None, out_t=False, aux_t=None):
     acc_dt = torch.promote_types(a.dtype, torch.float32)  # fp32 accumulation (fp64 stays fp64 for oracles)
     af, bf = a.to(acc_dt), b.to(acc_dt)
     if layout == "nt":
@@ -88,11 +95,15 @@ def _torch_gemm(a, b, layout, out, epi, act, aux, aux_out, alpha, beta, opt=None
         acc = af @ bf
     else:
         acc = af.t() @ bf
+    if out_t:
+        acc = acc.t()
     if epi == "store":
         r = alpha * acc
         if beta != 0.0:
             r = r + beta * out.to(acc_dt)
         out.copy_(r)
+        if aux_t is not None:
+            aux_t.copy_(out.t())
     elif epi == "act":
         if aux_out is not None:
             aux_out.copy_(acc)
@@ -264,26 +275,32 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
          alpha: float = 1.0, beta: float = 0.0, out_dtype: torch.dtype | None = None, group_m: int | None = None,
          force: str | None = None, lr: float = 0.0, betas: tuple = (0.9, 0.95), eps: float = 1e-8,
          wd: float = 0.0, step: int = 0, opt_m: torch.Tensor | None = None,
-         opt_v: torch.Tensor | None = None, mask: torch.Tensor | None = None) -> torch.Tensor:
+         opt_v: torch.Tensor | None = None, mask: torch.Tensor | None = None, out_t: bool = False,
+         aux_t: torch.Tensor | None = None) -> torch.Tensor:
     """``mask`` (ReLU only, GPU, see ``relu_mask_supported``): ``epi="act"`` also writes the activation-gradient
     bitmask, ``epi="dact"`` reads it instead of ``aux`` (1 bit instead of a bf16 per element).  CPU tensors
-    ignore it (``aux`` stays the source of truth there)."""
+    ignore it (``aux`` stays the source of truth there).  ``out_t`` / ``aux_t``: transposed outputs (module doc)."""
     M, N, K = gemm_shape(a, b, layout)
+    if out_t or aux_t is not None:
+        _check_transposed(a, layout, epi, M, N, K, out_t, aux_t, beta)
     if group_m is None:   # raster band height: the layout's policy (profiles/r3/group_m_sweep_r3.txt)
         group_m = _POLICY["group_m_nt"] if layout == "nt" else 4
     if a.dtype != b.dtype:
         raise TypeError(f"gemm operands differ in dtype: {a.dtype} vs {b.dtype}")
     nout = out_cols(N, epi)
+    oshape = (nout, M) if out_t else (M, nout)
     if out is None:
-        out = torch.empty((M, nout), dtype=out_dtype or a.dtype, device=a.device)
-    if out.shape != (M, nout):
-        raise ValueError(f"out has shape {tuple(out.shape)}, expected {(M, nout)}")
+        out = torch.empty(oshape, dtype=out_dtype or a.dtype, device=a.device)
+    if out.shape != oshape:
+        raise ValueError(f"out has shape {tuple(out.shape)}, expected {oshape}")
     if epi in ("dact", "dglu") and aux is None:
         raise ValueError(f"epilogue {epi} needs aux (pre-activation)")
     if epi == "glu" and N % 32:
         raise ValueError("gated GEMM needs N % 32 == 0 (16-row interleave)")
-    # fused optimizers: the weight-gradient layouts -- TN, or NN on 224-row tiles (transposed-activation TP layout)
-    opt_layout_ok = layout == "tn" or (layout == "nn" and use_m224(M, N) and a.device.type == "cuda")
+    # fused optimizers: the weight-gradient layouts -- TN, NN on 224-row tiles (transposed-activation TP layout), or
+    # the NN weight-gradient layout's 256x256 tiles (split masters)
+    opt_layout_ok = layout == "tn" or (layout == "nn" and a.device.type == "cuda" and (
+        use_m224(M, N) or (epi == "sgd_split" and nn_wgrad_supported(M, N, K))))
     if epi in ("sgd", "adam"):
         if not (opt_layout_ok or (layout == "nn" and a.device.type != "cuda")) or out.dtype != torch.float32:
             raise ValueError("fused-optimizer epilogues need the TN (weight-gradient) layout and an fp32 master")
@@ -302,7 +319,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
                              "bf16 working copy as aux_out")
     if a.device.type != "cuda":
         opt = {"lr": lr, "b1": betas[0], "b2": betas[1], "eps": eps, "wd": wd, "step": step, "m": opt_m, "v": opt_v}
-        return _torch_gemm(a, b, layout, out, epi, act, aux, aux_out, alpha, beta, opt)
+        return _torch_gemm(a, b, layout, out, epi, act, aux, aux_out, alpha, beta, opt, out_t, aux_t)
 
     for t, nm in ((a, "a"), (b, "b"), (out, "out")):
         _check_rowmajor(t, nm)
@@ -314,8 +331,17 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
         b6 = split3(b, 1, layout != "nt")
         return gemm(a6, b6, layout, out, epi=epi, act=act, aux=aux, aux_out=aux_out, alpha=alpha, beta=beta,
                     group_m=group_m, lr=lr, betas=betas, eps=eps, wd=wd, step=step, opt_m=opt_m, opt_v=opt_v)
+    code = EPIS[epi]
+    if out_t:
+        code = EPI_T[epi]
+    elif aux_t is not None:
+        code, aux_out = EPI_STORE_DT, aux_t
     auxt = aux if aux is not None else aux_out
-    if auxt is not None:
+    if aux_t is not None:
+        _check_rowmajor(aux_t, "aux_t")
+        if aux_t.dtype != out.dtype or aux_t.shape != (N, M):
+            raise ValueError(f"aux_t must be the [N, M] = {(N, M)} transposed output in the output dtype")
+    elif auxt is not None:
         _check_rowmajor(auxt, "aux")
         if epi in ("sgd", "adam", "sgd_split", "adam_split"):
             if auxt.dtype != torch.bfloat16 or auxt.shape != out.shape:
@@ -326,7 +352,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
     in_dt = _native.dtype_code(a.dtype)
     out_dt = _native.dtype_code(torch.bfloat16 if out.dtype == torch.int16 else out.dtype)  # 16-bit planes
     ksplit, ws = 1, None
-    if a.dtype == torch.bfloat16 and force in (None, "mfma_bf16"):
+    if a.dtype == torch.bfloat16 and force in (None, "mfma_bf16") and code == EPIS[epi]:
         ksplit = choose_ksplit(M, N, K)
         if ksplit > 1 and L.dllm_gemm_path(in_dt, out_dt, M, N, K, a.stride(0), b.stride(0), out.stride(0)) == 0:
             ws = _splitk_workspace(ksplit * M * N, a.device)
@@ -335,7 +361,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
     obs = _observe.active()
     if obs is not None:
         obs.gemm_begin()
-    rc = L.dllm_gemm(in_dt, out_dt, LAYOUTS[layout], EPIS[epi], act_code(act),
+    rc = L.dllm_gemm(in_dt, out_dt, LAYOUTS[layout], code, act_code(act),
                      a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), out.data_ptr(), out.stride(0),
                      aux.data_ptr() if aux is not None else None,
                      aux_out.data_ptr() if aux_out is not None else None,
@@ -351,6 +377,44 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
     if obs is not None:
         obs.gemm_end()
     return out
+
+
+EPI_T = {"store": 10, "sgd_split": 9}     # csrc/common.h EPI_STORE_T / EPI_SGDS_T
+EPI_STORE_DT = 11
+
+
+def nn_wgrad_supported(M: int, N: int, K: int) -> bool:
+    """Shapes of the NN weight-gradient layout's kernels (transposed outputs / copies, NN fused SGD): 256x256 output
+    tiles on the 8-phase kernel (K a multiple of its 128-deep step) and not the 224-row family."""
+    return M % 256 == 0 and N % 256 == 0 and K % 128 == 0 and not use_m224(M, N)
+
+
+def _check_transposed(a, layout, epi, M, N, K, out_t, aux_t, beta) -> None:
+    if out_t and aux_t is not None:
+        raise ValueError("out_t and aux_t are exclusive")
+    if out_t and (epi not in EPI_T or layout != "nn"):
+        raise ValueError(f"out_t: epilogues {sorted(EPI_T)} in the NN layout only (got {epi}, {layout})")
+    if aux_t is not None and (epi != "store" or layout not in ("nt", "nn")):
+        raise ValueError(f"aux_t: the store epilogue in the NT / NN layouts only (got {epi}, {layout})")
+    if beta != 0.0:
+        raise ValueError("transposed outputs: beta must be 0")
+    if a.device.type == "cuda" and (a.dtype != torch.bfloat16 or not nn_wgrad_supported(M, N, K)):
+        raise ValueError(f"transposed outputs need bf16 operands on 256x256 tiles with K % 128 == 0, got {(M, N, K)}")
+
+
+def transpose_bf16(src: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:
+    """``dst = srcᵀ`` for bf16 row-major views (rows and columns multiples of 64 on the GPU kernel)."""
+    R, C = src.shape
+    if dst.shape != (C, R) or src.dtype != dst.dtype:
+        raise ValueError(f"transpose: dst {tuple(dst.shape)} / {dst.dtype} for src {tuple(src.shape)} / {src.dtype}")
+    if src.device.type != "cuda":
+        dst.copy_(src.t())
+        return dst
+    _check_rowmajor(src, "src")
+    _check_rowmajor(dst, "dst")
+    _native.check(_native.lib().dllm_transpose_bf16(src.data_ptr(), src.stride(0), dst.data_ptr(), dst.stride(0), R, C,
+                                                    _native.stream_ptr(src.device)), "dllm_transpose_bf16")
+    return dst
 
 
 _PAIR = {"enabled": True}

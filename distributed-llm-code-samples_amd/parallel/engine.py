@@ -42,9 +42,8 @@ from dataclasses import dataclass
 
 import torch
 
-from ..models.ffn import (deinterleave_w13, interleave_w13, layer_bwd, layer_bwd_t, layer_fwd, layer_fwd_t,
-                          needs_preact,
-                          recompute_fwd1)
+from ..models.ffn import (NNWgrad, deinterleave_w13, interleave_w13, layer_bwd, layer_bwd_t, layer_fwd, layer_fwd_t,
+                          needs_preact, recompute_fwd1, wgrad_w1, wgrad_w2)
 from ..ops.elementwise import adam_split_step_, adam_step_, cast_, sgd_split_step_, sgd_step_
 from ..ops.master import join_flat, part_flat, split_master
 from ..utils import streams
@@ -386,6 +385,15 @@ class FFNTrainer:
             self.xs_full = [torch.empty((T, D), dtype=self.cd, device=dev) for _ in range(L)] if keep else None
             self.dyfull = torch.empty((T, D), dtype=self.cd, device=dev)
             self.dxs = [torch.empty((Tl, D), dtype=self.cd, device=dev) for _ in range(2)]
+        # NN weight-gradient layout (models/ffn.NNWgrad): transposed copies xᵀ of every layer input (the previous layer's
+        # fwd-2 epilogue writes them; layer 0's is transposed at the step start) and dyᵀ of every layer's output
+        # gradient (the layer above's dx epilogue, rotating with dxb; the top layer's is transposed at the step start)
+        self.wgrad_nn = self._wgrad_nn_supported()
+        self.xT = self.dxTb = self.dyT_top = None
+        if self.wgrad_nn:
+            self.xT = [torch.empty((D, T), dtype=self.cd, device=dev) for _ in range(L)]
+            self.dxTb = [torch.empty((D, T), dtype=self.cd, device=dev) for _ in range(len(self.dxb))]
+            self.dyT_top = torch.empty((D, T), dtype=self.cd, device=dev)
 
         # ---- DDP / ZeRO bucket state ----------------------------------------------------------------
         if self.ddp or self.zero:
@@ -406,6 +414,33 @@ class FFNTrainer:
             self.ag_pending = [None] * len(self.buckets)
             self.rs_issued_at = [None] * len(self.buckets)
         self._next_bucket = 0
+
+    def _wgrad_nn_supported(self) -> bool:
+        """Whether the weight gradients run in the NN layout (``cfg.wgrad_layout``; models/ffn.NNWgrad): GPU, bf16, the
+        plain row-major layer (no TP / SP / FSDP / transposed-activation mode / recompute / grouped pair / TP chunks),
+        256x256 8-phase shapes, and a fused optimizer only as SGD on split masters (stored gradients: any)."""
+        cfg = self.cfg
+        if cfg.wgrad_layout not in ("auto", "tn", "nn"):
+            raise ValueError(f"unknown wgrad_layout {cfg.wgrad_layout!r}")
+        if cfg.wgrad_layout == "tn":
+            return False
+        from ..ops.gemm import nn_wgrad_supported
+
+        T, D = self.T, self.D
+        why = []
+        if self.device.type != "cuda" or self.cd != torch.bfloat16:
+            why.append("GPU bf16 only")
+        if self.tp_comm or self.sp or self.fsdp or self.tmode or self.pair_wgrads or self.tp_chunks > 1:
+            why.append("row-major data-parallel / single-device layers only")
+        if cfg.recompute != "none":
+            why.append("kept activations only")
+        if self.fused_opt and not (self.split and cfg.optimizer == "sgd"):
+            why.append("fused optimizer: SGD on split masters only")
+        if not (nn_wgrad_supported(D, self.F_loc, T) and nn_wgrad_supported(D, self.R1, T) and T % 64 == 0):
+            why.append(f"shapes (D={D}, F={self.F_loc}, T={T}) off the 256x256 8-phase tiles")
+        if why and cfg.wgrad_layout == "nn":
+            raise ValueError("wgrad_layout nn: " + "; ".join(why))
+        return not why
 
     # ------------------------------------------------------------------------------------------------
     # views
@@ -501,12 +536,15 @@ class FFNTrainer:
     def grad_view(self, l: int, name: str) -> torch.Tensor:
         return self._view(self.grads, self.entry[(l, name)])
 
-    def _layer_bwd_concurrent(self, l, g, w1, w2, a, h, kw1, kw2, need_dx):
+    def _layer_bwd_concurrent(self, l, g, w1, w2, a, h, kw1, kw2, need_dx, gT=None):
         """One layer's backward with the weight-gradient GEMMs on ``wg_stream`` (same math and order per
         stream as ``layer_bwd``).  Edges: dW2 after da (da reads the W2 copy dW2's fused update rewrites),
-        dW1 after dx (same for W1); buffers are reused only after the side stream's last read of them."""
+        dW1 after dx (same for W1); buffers are reused only after the side stream's last read of them.
+        ``gT`` (NN weight-gradient layout): gᵀ [D, T]; dx's epilogue then also writes dxᵀ into ``dxTb[j]``, which
+        rotates (and is released) with ``dxb[j]``.  Returns (the next layer's g, its gᵀ or None)."""
         from ..ops.gemm import gemm
 
+        nn = None
         main, side = torch.cuda.current_stream(self.device), self.wg_stream
         act = self.act
         da = self.da_ring[l % 2]
@@ -519,27 +557,31 @@ class FFNTrainer:
         e_da = torch.cuda.Event()
         e_da.record(main)
         side.wait_event(e_da)
+        j = l % 3
+        if gT is not None:
+            nn = NNWgrad(self.xT[l], gT, self.dxTb[j] if need_dx else None)
         if need_dx:
             with torch.cuda.stream(side):
-                gemm(g, a, "tn", **kw2)                                   # dW2 = dyᵀ·a
+                wgrad_w2(g, a, kw2, nn)                                   # dW2 = dyᵀ·a
                 e_dy = torch.cuda.Event()
                 e_dy.record(side)
-            j = l % 3
             if self.dx_free[j] is not None:
                 main.wait_event(self.dx_free[j])
-            dx = gemm(da, w1, "nn", out=self.dxb[j])                     # dx = da·W1
-            self.dx_free[(l + 1) % 3] = e_dy                              # g (= dx of layer l+1) read
+            dx = gemm(da, w1, "nn", out=self.dxb[j], aux_t=nn.dx_t if nn is not None else None)   # dx = da·W1
+            self.dx_free[(l + 1) % 3] = e_dy                              # g / gᵀ (= dx of layer l+1) read
             e_dx = torch.cuda.Event()
             e_dx.record(main)
             side.wait_event(e_dx)
         with torch.cuda.stream(side):
-            gemm(da, self.xs[l], "tn", **kw1)                             # dW1 = daᵀ·x
+            wgrad_w1(da, self.xs[l], kw1, nn)                             # dW1 = daᵀ·x
             if not need_dx:
-                gemm(g, a, "tn", **kw2)                                   # layer 0: dW2 last
+                wgrad_w2(g, a, kw2, nn)                                   # layer 0: dW2 last
             e_w = torch.cuda.Event()
             e_w.record(side)
         self.da_free[l % 2] = e_w
-        return dx if need_dx else g
+        if need_dx:
+            return dx, (nn.dx_t if nn is not None else None)
+        return g, None
 
     def _mask(self, l: int) -> torch.Tensor | None:
         if self.masks is None:
@@ -1022,6 +1064,13 @@ class FFNTrainer:
             x = x[r * self.Tl:(r + 1) * self.Tl]
             dy = dy[r * self.Tl:(r + 1) * self.Tl]
         self.xs[0] = x
+        if self.wgrad_nn:
+            # the NN weight-gradient layout's transposed copies of the step's inputs (every other layer's come out of
+            # the producing GEMM epilogues): layer 0's xᵀ and the top layer's dyᵀ
+            from ..ops.gemm import transpose_bf16
+
+            transpose_bf16(x, self.xT[0])
+            transpose_bf16(dy, self.dyT_top)
 
         # ---------------- forward ----------------
         mark = self._mark("forward")
@@ -1079,7 +1128,7 @@ class FFNTrainer:
                     layer_fwd_t(self.xs[l], w1, w2, act, a, h, self.xs[l + 1], before_fwd2=before2, mask=self._mask(l))
                 else:
                     layer_fwd(self.xs[l], w1, w2, act, gated, a, h, self.xs[l + 1], before_fwd2=before2,
-                              mask=self._mask(l))
+                              mask=self._mask(l), y_t=self.xT[l + 1] if self.wgrad_nn and l + 1 < L else None)
                 if self.tp_comm:
                     last = l == L - 1
                     if self.tp_car is not None:
@@ -1112,6 +1161,7 @@ class FFNTrainer:
             # optimizer runs, so the reference's re-gather of L-2 (:245) is skipped when still resident
             self._fsdp_gather(L - 2)
         g = dy
+        gT = self.dyT_top if self.wgrad_nn else None    # gᵀ: the NN weight-gradient layout's dW2 operand
         for l in reversed(range(L)):
             if self.fsdp:
                 if l < L - 1:
@@ -1155,7 +1205,7 @@ class FFNTrainer:
                         w.wait()
                     g = self.dxs[l % 2]
             elif self.wg_stream is not None:
-                g = self._layer_bwd_concurrent(l, g, w1, w2, a, h, gw1, gw2, need_dx)
+                g, gT = self._layer_bwd_concurrent(l, g, w1, w2, a, h, gw1, gw2, need_dx, gT)
             elif self.tmode:
                 dx = layer_bwd_t(g, self.xs[l], w1, w2, act, a, h, gw1, gw2, self.da,
                                  self.dxb[l % 2] if need_dx else None, hooks, mask=self._mask(l))
@@ -1164,11 +1214,13 @@ class FFNTrainer:
             else:
                 if not keep:
                     recompute_fwd1(self.xs[l], w1, act, gated, a, h, mask=self._mask(l))
+                nn = NNWgrad(self.xT[l], gT, self.dxTb[l % 2] if need_dx else None) if self.wgrad_nn else None
                 dx = layer_bwd(g, self.xs[l], w1, w2, act, gated, a, h, gw1, gw2, self.da,
                                self.dxb[l % 2] if need_dx else None, hooks, mask=self._mask(l),
-                               dx_first=self.tp_comm and cfg.tp_overlap, pair_wgrads=self.pair_wgrads)
+                               dx_first=self.tp_comm and cfg.tp_overlap, pair_wgrads=self.pair_wgrads, nn=nn)
                 if dx is not None:
                     g = dx
+                    gT = nn.dx_t if nn is not None else None
             if self.zero:
                 # reduce-scatters issued during an earlier layer have had a full layer of compute to
                 # finish: update those shards now (1/dp of the optimizer work, off the tail), on the side stream

@@ -43,7 +43,7 @@ def config_from_args(a) -> TrainConfig:
                        random_seed=a.random_seed, dtype=a.dtype, grad_dtype=a.grad_dtype or a.dtype,
                        optimizer=a.optimizer, lr=a.lr, weight_decay=a.weight_decay,
                        sequence_parallel=a.sequence_parallel, recompute=a.recompute, bucket_mb=a.bucket_mb,
-                       data=a.data, comm_backend=a.comm, debug_sync=a.debug_sync, tp_allreduce=a.tp_allreduce,
+                       data=a.data, comm_backend=a.comm, debug_sync=a.debug_sync, tp_allreduce=a.tp_allreduce, wgrad_layout=a.wgrad_layout,
                        fp32_gemm=a.fp32_gemm, master=a.master)
 
 

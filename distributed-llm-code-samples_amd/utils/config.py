@@ -68,10 +68,15 @@ class TrainConfig:
                                      # runs while chunk i+1 computes, and the next layer's chunk i starts as
                                      # soon as that one all-reduce is done (1 = one all-reduce per layer)
     relu_mask: bool = True           # ReLU: the dgrad reads a 1-bit activation mask written by the forward
+                                     # GEMM instead of the bf16 activation (GPU, 8-phase kernel shapes)
     # GPU, F/tp a multiple of 224 whose 224-row tile grid fills the chip better (the MP config at tp = 8): keep activations as [F, T] and W2 as W2ᵀ so
     # every F-sized GEMM dimension runs on 224-row tiles that fill the chip (models/ffn.layer_fwd_t / layer_bwd_t)
     tp_transposed: bool = True
-                                     # GEMM instead of the bf16 activation (GPU, 8-phase kernel shapes)
+    # weight-gradient GEMM layout: "tn" (dW = dyᵀ·a, daᵀ·x: both operands through transposed LDS reads) or "nn"
+    # (transposed copies xᵀ / dyᵀ [D, T] from the producing epilogues; models/ffn.NNWgrad); "auto" = nn where the
+    # engine supports it (GPU, bf16, 256x256 8-phase shapes, no TP / SP / FSDP / recompute, SGD on split masters or
+    # stored gradients)
+    wgrad_layout: str = "auto"
     wgrad_stream: bool = False       # single device, fused optimizer: weight-gradient GEMMs on a second
                                      # stream, concurrent with the dgrad chain (CUs shared; epilogues overlap)
     wgrad_stream_max_tpc: float = 4.0  # wgrad_stream only while a weight gradient has <= this many 256x256 tiles
@@ -138,6 +143,8 @@ def add_extended_args(p: argparse.ArgumentParser) -> None:
                    help="communicator implementation for the role groups (native = C++ RCCL layer)")
     p.add_argument("--tp_allreduce", choices=["rccl", "custom", "auto"], default="rccl",
                    help="TP activation all-reduce: RCCL or the custom two-shot xGMI peer all-reduce")
+    p.add_argument("--wgrad_layout", choices=["auto", "tn", "nn"], default="auto",
+                   help="weight-gradient GEMM layout (nn: transposed xᵀ / dyᵀ copies from the producing epilogues)")
     p.add_argument("--nprocs", type=int, default=0, help="ranks to spawn (0 = all visible GPUs)")
     p.add_argument("--dp", type=int, default=0)
     p.add_argument("--tp", type=int, default=0)

@@ -1,0 +1,115 @@
+"""The NN weight-gradient layout against the TN one on the flagship layer (T = 8192, D = 4096, F = 16384), per GEMM:
+
+* dW2 [D, F]: TN ``dyᵀ·a`` fused split-master SGD  vs  NN ``(dyᵀ)·a`` with ``dyᵀ`` [D, T] stored (A K-contiguous)
+* dW1 [F, D]: TN ``daᵀ·x``                          vs  NN ``(xᵀ)·da`` written transposed into W1 (``out_t``)
+* the producers of the transposed copies: y = a·W2ᵀ (NT) and dx = da·W1 (NN) with and without ``aux_t``, and the
+  standalone transpose of a [T, D] bf16 matrix (layer 0's x, the top layer's dy)
+
+Every pair is checked bitwise (same fp32 master before, same master after) before it is timed.  Interleaved rounds,
+median of rounds, microseconds.
+
+    python scripts/bench_nn_wgrad.py [--iters 10 --rounds 5]"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import dllm  # noqa: E402,F401
+from dllm.ops.gemm import gemm, transpose_bf16  # noqa: E402
+from dllm.ops.master import split_master  # noqa: E402
+
+
+def timeit(fn, iters):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args()
+    T, D, F = 8192, 4096, 16384
+    g = torch.Generator().manual_seed(0)
+    bf = torch.bfloat16
+
+    def rnd(*shape, s=1.0):
+        return (torch.randn(*shape, generator=g) * s).to(bf).cuda()
+
+    da, x, dy, act = rnd(T, F), rnd(T, D), rnd(T, D), rnd(T, F)
+    w1, w2 = rnd(F, D, s=0.02), rnd(D, F, s=0.02)
+    xT, dyT = x.t().contiguous(), dy.t().contiguous()
+    m1 = (torch.randn(F, D, generator=g) * 0.02).cuda()
+    m2 = (torch.randn(D, F, generator=g) * 0.02).cuda()
+    hi1, lo1 = split_master(m1)
+    hi2, lo2 = split_master(m2)
+    h1b, l1b, h2b, l2b = hi1.clone(), lo1.clone(), hi2.clone(), lo2.clone()
+    lr = 1e-3
+
+    checks = {}
+    # bitwise: one update each way from the same master
+    gemm(da, x, "tn", out=lo1, epi="sgd_split", lr=lr, aux_out=hi1)
+    gemm(xT, da, "nn", out=l1b, epi="sgd_split", lr=lr, aux_out=h1b, out_t=True)
+    checks["dW1 nn out_t == tn"] = bool(torch.equal(hi1, h1b) and torch.equal(lo1, l1b))
+    gemm(dy, act, "tn", out=lo2, epi="sgd_split", lr=lr, aux_out=hi2)
+    gemm(dyT, act, "nn", out=l2b, epi="sgd_split", lr=lr, aux_out=h2b)
+    checks["dW2 nn == tn"] = bool(torch.equal(hi2, h2b) and torch.equal(lo2, l2b))
+    y0, y1, yT = (torch.empty(T, D, dtype=bf, device="cuda") for _ in range(3))
+    yT = torch.empty(D, T, dtype=bf, device="cuda")
+    gemm(act, w2, "nt", out=y0)
+    gemm(act, w2, "nt", out=y1, aux_t=yT)
+    checks["y with aux_t == y"] = bool(torch.equal(y0, y1))
+    checks["yT == y.t()"] = bool(torch.equal(yT, y0.t()))
+    dx0, dx1, dxT = torch.empty(T, D, dtype=bf, device="cuda"), torch.empty(T, D, dtype=bf, device="cuda"), \
+        torch.empty(D, T, dtype=bf, device="cuda")
+    gemm(da, w1, "nn", out=dx0)
+    gemm(da, w1, "nn", out=dx1, aux_t=dxT)
+    checks["dx with aux_t == dx"] = bool(torch.equal(dx0, dx1))
+    checks["dxT == dx.t()"] = bool(torch.equal(dxT, dx0.t()))
+    tT = torch.empty(D, T, dtype=bf, device="cuda")
+    transpose_bf16(x, tT)
+    checks["transpose"] = bool(torch.equal(tT, xT))
+    print("bitwise:", json.dumps(checks), flush=True)
+
+    cases = {
+        "dW1_tn_sgd": lambda: gemm(da, x, "tn", out=lo1, epi="sgd_split", lr=1e-9, aux_out=hi1),
+        "dW1_nn_t_sgd": lambda: gemm(xT, da, "nn", out=lo1, epi="sgd_split", lr=1e-9, aux_out=hi1, out_t=True),
+        "dW2_tn_sgd": lambda: gemm(dy, act, "tn", out=lo2, epi="sgd_split", lr=1e-9, aux_out=hi2),
+        "dW2_nn_sgd": lambda: gemm(dyT, act, "nn", out=lo2, epi="sgd_split", lr=1e-9, aux_out=hi2),
+        "y_nt": lambda: gemm(act, w2, "nt", out=y0),
+        "y_nt_aux_t": lambda: gemm(act, w2, "nt", out=y1, aux_t=yT),
+        "dx_nn": lambda: gemm(da, w1, "nn", out=dx0),
+        "dx_nn_aux_t": lambda: gemm(da, w1, "nn", out=dx1, aux_t=dxT),
+        "transpose_TxD": lambda: transpose_bf16(x, tT),
+    }
+    res = {k: [] for k in cases}
+    for _ in range(a.rounds):
+        for k, fn in cases.items():
+            res[k].append(timeit(fn, a.iters))
+    med = {k: round(statistics.median(v), 1) for k, v in res.items()}
+    for k, v in med.items():
+        print(f"{k:16s} {v:8.1f} us", flush=True)
+    per_layer_old = med["dW1_tn_sgd"] + med["dW2_tn_sgd"] + med["y_nt"] + med["dx_nn"]
+    per_layer_new = med["dW1_nn_t_sgd"] + med["dW2_nn_sgd"] + med["y_nt_aux_t"] + med["dx_nn_aux_t"]
+    print(f"per middle layer (dW1 + dW2 + y + dx): TN {per_layer_old:.1f} us, NN layout {per_layer_new:.1f} us "
+          f"({per_layer_new - per_layer_old:+.1f}); + 2 transposes per step {2 * med['transpose_TxD']:.1f} us",
+          flush=True)
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump({"checks": checks, "median_us": med}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

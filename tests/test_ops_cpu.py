@@ -162,3 +162,51 @@ def test_engine_cpu_has_no_device_side_buffers():
                       wgrad_stream=True)
     eng = FFNTrainer(cfg, Mesh(), torch.device("cpu"))
     assert eng.masks is None and eng.wg_stream is None
+
+
+def test_transposed_outputs_reference_cpu():
+    """``out_t`` / ``aux_t`` (the NN weight-gradient layout) on the torch reference: out_t writes Cᵀ, aux_t a
+    transposed copy next to the plain store; the NN-layout layer backward equals the TN one."""
+    from dllm.models.ffn import NNWgrad
+    from dllm.ops.gemm import transpose_bf16
+
+    g = torch.Generator().manual_seed(0)
+    T, D, F = 64, 32, 96
+    x, da, dy, a = (torch.randn(*s, generator=g) for s in ((T, D), (T, F), (T, D), (T, F)))
+    torch.testing.assert_close(gemm(x.t().contiguous(), da, "nn", out_t=True), gemm(da, x, "tn"))
+    yT = torch.empty(D, T)
+    w2 = torch.randn(D, F, generator=g)
+    y = gemm(a, w2, "nt", aux_t=yT)
+    assert torch.equal(yT, y.t())
+    xt = torch.empty(D, T)
+    assert torch.equal(transpose_bf16(x, xt), x.t())
+    w1 = torch.randn(F, D, generator=g)
+    ref, nn = [], []
+    for mode in (None, "nn"):
+        gw1, gw2 = torch.zeros(F, D), torch.zeros(D, F)
+        dx_t = torch.empty(D, T)
+        h = x @ w1.t()
+        act = torch.relu(h)
+        kw = {} if mode is None else {"nn": NNWgrad(x.t().contiguous(), dy.t().contiguous(), dx_t)}
+        dx = layer_bwd(dy, x, w1, w2, "relu", False, act, None, gw1, gw2, torch.empty(T, F), torch.empty(T, D), **kw)
+        (ref if mode is None else nn).extend([gw1, gw2, dx])
+        if mode == "nn":
+            assert torch.equal(dx_t, dx.t())
+    for r, n in zip(ref, nn):
+        torch.testing.assert_close(n, r)
+
+
+def test_wgrad_layout_nn_needs_gpu():
+    import pytest
+
+    from dllm.parallel.engine import FFNTrainer
+    from dllm.parallel.mesh import Mesh
+
+    m = ModelConfig(model_size=256, ffn_dim=512, layers=1)
+    for layout, ok in (("auto", True), ("tn", True), ("nn", False)):
+        cfg = TrainConfig(model=m, batch_size=1, seq_len=256, wgrad_layout=layout)
+        if ok:
+            assert not FFNTrainer(cfg, Mesh(), torch.device("cpu")).wgrad_nn
+        else:
+            with pytest.raises(ValueError, match="wgrad_layout nn"):
+                FFNTrainer(cfg, Mesh(), torch.device("cpu"))

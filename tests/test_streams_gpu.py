@@ -115,3 +115,45 @@ def test_role_communicators_on_distinct_queues(backend):
     if backend == "torch":
         assert out["delay_own_ms"] > 40.0, out
         assert out["delay_other_ms"] < 30.0, out
+
+
+ENGINE_SCRIPT = r"""
+import json, torch
+import dllm
+from dllm.models.ffn import init_ffn_params_device
+from dllm.parallel.engine import FFNTrainer
+from dllm.parallel.mesh import Mesh
+from dllm.utils import streams
+from dllm.utils.config import ModelConfig, TrainConfig
+from dllm.utils.data import DeviceMockData
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(0)
+m = ModelConfig(model_size=4096, ffn_dim=16384, layers=1, act="relu")     # flagship layer: weight-gradient stream on
+cfg = TrainConfig(model=m, batch_size=1, seq_len=1024, dtype="bf16", grad_dtype="fp32", optimizer="sgd")
+eng = FFNTrainer(cfg, Mesh(), dev)          # no bench.py, no launcher: the engine reserves the queue itself
+eng.load_full_params(init_ffn_params_device(m.D, m.F, m.layers, 1, dev))
+data = DeviceMockData(cfg.tokens, m.D, torch.bfloat16, dev)
+for i in range(3):
+    x, dy = data.fill(i)
+    eng.train_step(x, dy)
+torch.cuda.synchronize()
+side = {"wgrad": eng.wg_stream, "opt": getattr(eng, "opt_stream", None), "data": getattr(data, "_stream", None)}
+side = {k: v for k, v in side.items() if v is not None}
+print("JSON" + json.dumps({"sides": sorted(side), "report": streams.queue_report(0, side)}))
+"""
+
+
+def test_single_rank_engine_reserves_compute_queue():
+    """a world==1 run that goes through neither bench.py nor the launcher (the Python API, train_ffns at
+    N=1) still gets the compute-queue reservation -- FFNTrainer makes it before creating any side stream -- so at
+    HIP's default 4 queues no side stream and no pool stream shares the compute stream's queue."""
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    env.pop("GPU_MAX_HW_QUEUES", None)
+    r = subprocess.run([sys.executable, "-c", ENGINE_SCRIPT], capture_output=True, text=True, timeout=300, cwd=ROOT,
+                       env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("JSON")][0][4:])
+    assert "wgrad" in out["sides"], out
+    rep = out["report"]
+    assert rep["compute_queue_exclusive"], rep
+    assert rep["side_streams_on_compute_queue"] == [] and rep["pool_streams_on_compute_queue"] == 0, rep
