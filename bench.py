@@ -180,7 +180,7 @@ def parse(argv=None):
                         "update into the wgrad GEMM epilogue)")
     p.add_argument("--phases", action="store_true",
                    help="also report per-phase GPU time (forward / backward / optimizer tail) from HIP events")
-    p.add_argument("--wgrad_layout", choices=["auto", "tn", "nn"], default="auto",
+    p.add_argument("--wgrad_layout", choices=["auto", "tn", "nn", "nn_w1"], default="auto",
                    help="weight-gradient GEMM layout: nn = transposed xᵀ / dyᵀ copies written by the producing "
                         "epilogues, both weight gradients as NN GEMMs with a K-contiguous A (models/ffn.NNWgrad); "
                         "auto = nn wherever the engine supports it")
@@ -451,7 +451,7 @@ def _run_on_mesh(a, method, cfg, mesh, n, world, dev, steps, warmup, force_comm,
            "wgrad_stream": eng.wg_stream is not None,
            # small-grid weight gradients in one grouped launch / F-major activations on 224-row tiles (MP at tp 8)
            "pair_wgrads": bool(eng.pair_wgrads), "tp_transposed": bool(eng.tmode),
-           "wgrad_nn": bool(eng.wgrad_nn),
+           "wgrad_nn": bool(eng.wgrad_nn), "wgrad_nn_w2": bool(eng.wgrad_nn_w2),
            # the ranks each role communicator actually spans (RCCL / gloo group sizes; {} = no collective)
            "comm_sizes": {role: g.size() for role, g in mesh.groups.items() if g is not None}}
     if eng.tp_ar_choice is not None:
@@ -524,7 +524,7 @@ def _run_on_mesh(a, method, cfg, mesh, n, world, dev, steps, warmup, force_comm,
 
 SIDE_KEYS = ("value", "ms_per_step", "tflops_per_gpu", "peak_hbm_gib", "parallelism", "model", "global_batch",
              "steps", "warmup", "warmup_ms", "timed_ms", "finite", "state_gib", "comm", "queues", "comm_sizes",
-             "pair_wgrads", "tp_transposed", "wgrad_nn", "tp_allreduce_choice")
+             "pair_wgrads", "tp_transposed", "wgrad_nn", "wgrad_nn_w2", "tp_allreduce_choice")
 
 
 def main(argv=None) -> int:
@@ -603,7 +603,7 @@ def main(argv=None) -> int:
             "comm_backend": a.comm, "hip_graph": bool(a.graph), "gemm_variant": a.gemm_variant,
             "tp_allreduce": a.tp_allreduce, "wgrad_stream": head.get("wgrad_stream", False),
             "pair_wgrads": head.get("pair_wgrads", False), "tp_transposed": head.get("tp_transposed", False),
-            "wgrad_nn": head.get("wgrad_nn", False),
+            "wgrad_nn": head.get("wgrad_nn", False), "wgrad_nn_w2": head.get("wgrad_nn_w2", False),
         }
         for k in ("comm", "phase_ms_per_step", "queues", "collectives_elided"):
             if k in head:

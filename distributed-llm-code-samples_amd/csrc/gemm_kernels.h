@@ -2148,14 +2148,15 @@ static hipError_t dispatch_x(int epi, const GemmArgs& a, int out_dt, hipStream_t
       if (f32) return hipErrorInvalidValue;
       launch_8ph_act<L, EPI_STORE_DT, uint16_t, -1, 8>(a, nb, s);
       break;
-    case EPI_STORE_T:
+    case EPI_STORE_T:   // any layout (the NT / TN instantiations serve operand-order experiments and tests)
+      if (f32) launch_8ph_act<L, EPI_STORE_T, float, -1, 8>(a, nb, s);
+      else launch_8ph_act<L, EPI_STORE_T, uint16_t, -1, 8>(a, nb, s);
+      break;
     case EPI_SGDS_T:
     case EPI_SGDS:
       if constexpr (L == L_NN) {
         if (epi == EPI_SGDS) launch_8ph_act<L, EPI_SGDS, float, -1, 8>(a, nb, s);
-        else if (epi == EPI_SGDS_T) launch_8ph_act<L, EPI_SGDS_T, float, -1, 8>(a, nb, s);
-        else if (f32) launch_8ph_act<L, EPI_STORE_T, float, -1, 8>(a, nb, s);
-        else launch_8ph_act<L, EPI_STORE_T, uint16_t, -1, 8>(a, nb, s);
+        else launch_8ph_act<L, EPI_SGDS_T, float, -1, 8>(a, nb, s);
         break;
       } else {
         return hipErrorInvalidValue;
@@ -2348,5 +2349,6 @@ hipError_t dispatch_nn_pair(int epi, const GemmArgs& a0, const GemmArgs& a1, int
 hipError_t dispatch_nn_opt(int epi, const GemmArgs& a, hipStream_t s);
 hipError_t dispatch_nt_x(int epi, const GemmArgs& a, int out_dt, hipStream_t s);
 hipError_t dispatch_nn_x(int epi, const GemmArgs& a, int out_dt, hipStream_t s);
+hipError_t dispatch_tn_x(int epi, const GemmArgs& a, int out_dt, hipStream_t s);
 
 }  // namespace dllm

@@ -19,4 +19,7 @@ hipError_t dispatch_tn_pair(int epi, const GemmArgs& a0, const GemmArgs& a1, int
   return dispatch_pair<L_TN, BT_M>(epi, a0, a1, out_dt, s);
 }
 
+// transposed plain store (operand-order experiments, tests): gemm_kernels.h dispatch_x
+hipError_t dispatch_tn_x(int epi, const GemmArgs& a, int out_dt, hipStream_t s) { return dispatch_x<L_TN>(epi, a, out_dt, s); }
+
 }  // namespace dllm

@@ -119,14 +119,15 @@ class NNWgrad(NamedTuple):
     operands -- ``x_t`` = xᵀ [D, T] (the previous layer's fwd-2 epilogue writes it, ``layer_fwd(y_t=)``) and ``dy_t``
     = dyᵀ [D, T] (the layer above's dx epilogue writes it, ``dx_t``) -- both run as NN GEMMs with a K-contiguous A:
     ``dW2 = (dyᵀ)·a`` [D, F] and ``dW1ᵀ = (xᵀ)·da`` [D, F] written transposed into W1 [F, D] (``gemm(out_t=True)``).
-    Same products, same accumulation order: bitwise the TN results (tests/test_gemm_nnwgrad_gpu.py)."""
+    Same products, same accumulation order: bitwise the TN results (tests/test_gemm_nnwgrad_gpu.py).  ``dy_t`` None:
+    dW2 stays TN (and dx needs no transposed copy) -- the ``nn_w1`` mode."""
     x_t: torch.Tensor
-    dy_t: torch.Tensor
+    dy_t: torch.Tensor | None
     dx_t: torch.Tensor | None
 
 
 def wgrad_w2(dy: torch.Tensor, a: torch.Tensor, kw2: dict, nn: NNWgrad | None) -> None:
-    if nn is None:
+    if nn is None or nn.dy_t is None:
         gemm(dy, a, "tn", **kw2)                                      # dW2 = dyᵀ·a        [D, F]
     else:
         gemm(nn.dy_t, a, "nn", **kw2)                                 # dW2 = (dyᵀ)·a      [D, F]

@@ -24,7 +24,8 @@ followed by an epilogue:
 
 Transposed outputs (the NN weight-gradient layout, ``ffn.layer_bwd(..., wgrad_nn=...)``; 256x256 8-phase tiles):
 
-* ``out_t=True`` (``"store"``, ``"sgd_split"``, layout ``"nn"``): ``out`` (and ``aux_out``) hold ``Cᵀ`` [N, M] -- e.g.
+* ``out_t=True`` (``"store"`` in any layout, ``"sgd_split"`` in ``"nn"``): ``out`` (and ``aux_out``) hold ``Cᵀ``
+  [N, M] -- e.g.
   ``dW1ᵀ = xᵀ·da`` written into (or updating) ``W1`` [F, D] while ``xᵀ`` is the K-contiguous A operand
 * ``aux_t=`` (``"store"``, beta 0, bf16, layouts ``"nt"`` / ``"nn"``): also writes ``Cᵀ`` [N, M] into ``aux_t`` --
   e.g. a layer's output ``y`` and its ``yᵀ``, the next layer's K-contiguous weight-gradient operand
@@ -392,8 +393,8 @@ def nn_wgrad_supported(M: int, N: int, K: int) -> bool:
 def _check_transposed(a, layout, epi, M, N, K, out_t, aux_t, beta) -> None:
     if out_t and aux_t is not None:
         raise ValueError("out_t and aux_t are exclusive")
-    if out_t and (epi not in EPI_T or layout != "nn"):
-        raise ValueError(f"out_t: epilogues {sorted(EPI_T)} in the NN layout only (got {epi}, {layout})")
+    if out_t and (epi not in EPI_T or (epi != "store" and layout != "nn")):
+        raise ValueError(f"out_t: 'store' (any layout) or 'sgd_split' (NN layout) only (got {epi}, {layout})")
     if aux_t is not None and (epi != "store" or layout not in ("nt", "nn")):
         raise ValueError(f"aux_t: the store epilogue in the NT / NN layouts only (got {epi}, {layout})")
     if beta != 0.0:

@@ -38,6 +38,8 @@ MI355X-first memory design (288 GB HBM per GPU):
 """
 from __future__ import annotations
 
+import contextlib
+import os
 from dataclasses import dataclass
 
 import torch
@@ -52,6 +54,8 @@ from . import comm
 from .mesh import Mesh
 
 ALIGN = 64  # elements; keeps every view 128/256-B aligned for the LDS-DMA GEMM operand loads
+# NN weight-gradient layout: transpose the step's x / dy on the weight-gradient stream (1) or the compute stream (0)
+_TRANSPOSE_ON_SIDE = os.environ.get("DLLM_NN_TRANSPOSE_SIDE", "1") != "0"
 
 
 def _round_up(n: int, a: int) -> int:
@@ -366,12 +370,19 @@ class FFNTrainer:
             from ..ops.gemm import pair_supported
 
             self.pair_wgrads = pair_supported(((D, self.F_loc, T), (self.R1, D, T)), self.cd)
+        # NN weight-gradient layout (models/ffn.NNWgrad; buffers below).  It runs the backward serially: with the
+        # concurrent weight-gradient stream it measured 0.35-0.45 ms per step slower than serial (3 interleaved pairs,
+        # profiles/r5/nn_wgrad_step_ab_r5.txt), serial NN 0.1-0.4 ms faster than the TN layout on the stream
+        # (DLLM_NN_CONCURRENT=1 keeps the stream for A/B runs)
+        mode = "nn_w1" if cfg.wgrad_layout == "auto" else cfg.wgrad_layout
+        self.wgrad_nn = self._wgrad_nn_supported() and mode in ("nn", "nn_w1")   # dW1 as NN (out_t)
+        self.wgrad_nn_w2 = self.wgrad_nn and mode == "nn"                          # dW2 as NN too
         self.wg_stream = None
         wg_tiles = -(-self.R1 // 256) * -(-D // 256)
         ncu = torch.cuda.get_device_properties(dev).multi_processor_count if dev.type == "cuda" else 256
         if (cfg.wgrad_stream and self.fused_opt and dev.type == "cuda" and not self.tp_comm and not self.sp
                 and cfg.recompute == "none" and wg_tiles <= cfg.wgrad_stream_max_tpc * ncu and not self.pair_wgrads
-                and not self.tmode):
+                and not self.tmode and (not self.wgrad_nn or os.environ.get("DLLM_NN_CONCURRENT", "0") == "1")):
             self.wg_stream = self._side_stream("wgrad")
             self.da_ring = [self.da, torch.empty_like(self.da)]
             self.da_free = [None, None]
@@ -388,10 +399,10 @@ class FFNTrainer:
         # NN weight-gradient layout (models/ffn.NNWgrad): transposed copies xᵀ of every layer input (the previous layer's
         # fwd-2 epilogue writes them; layer 0's is transposed at the step start) and dyᵀ of every layer's output
         # gradient (the layer above's dx epilogue, rotating with dxb; the top layer's is transposed at the step start)
-        self.wgrad_nn = self._wgrad_nn_supported()
         self.xT = self.dxTb = self.dyT_top = None
         if self.wgrad_nn:
             self.xT = [torch.empty((D, T), dtype=self.cd, device=dev) for _ in range(L)]
+        if self.wgrad_nn_w2:
             self.dxTb = [torch.empty((D, T), dtype=self.cd, device=dev) for _ in range(len(self.dxb))]
             self.dyT_top = torch.empty((D, T), dtype=self.cd, device=dev)
 
@@ -420,7 +431,7 @@ class FFNTrainer:
         plain row-major layer (no TP / SP / FSDP / transposed-activation mode / recompute / grouped pair / TP chunks),
         256x256 8-phase shapes, and a fused optimizer only as SGD on split masters (stored gradients: any)."""
         cfg = self.cfg
-        if cfg.wgrad_layout not in ("auto", "tn", "nn"):
+        if cfg.wgrad_layout not in ("auto", "tn", "nn", "nn_w1"):
             raise ValueError(f"unknown wgrad_layout {cfg.wgrad_layout!r}")
         if cfg.wgrad_layout == "tn":
             return False
@@ -438,8 +449,8 @@ class FFNTrainer:
             why.append("fused optimizer: SGD on split masters only")
         if not (nn_wgrad_supported(D, self.F_loc, T) and nn_wgrad_supported(D, self.R1, T) and T % 64 == 0):
             why.append(f"shapes (D={D}, F={self.F_loc}, T={T}) off the 256x256 8-phase tiles")
-        if why and cfg.wgrad_layout == "nn":
-            raise ValueError("wgrad_layout nn: " + "; ".join(why))
+        if why and cfg.wgrad_layout in ("nn", "nn_w1"):
+            raise ValueError(f"wgrad_layout {cfg.wgrad_layout}: " + "; ".join(why))
         return not why
 
     # ------------------------------------------------------------------------------------------------
@@ -558,8 +569,8 @@ class FFNTrainer:
         e_da.record(main)
         side.wait_event(e_da)
         j = l % 3
-        if gT is not None:
-            nn = NNWgrad(self.xT[l], gT, self.dxTb[j] if need_dx else None)
+        if self.wgrad_nn:
+            nn = NNWgrad(self.xT[l], gT, self.dxTb[j] if need_dx and self.wgrad_nn_w2 else None)
         if need_dx:
             with torch.cuda.stream(side):
                 wgrad_w2(g, a, kw2, nn)                                   # dW2 = dyᵀ·a
@@ -1066,11 +1077,18 @@ class FFNTrainer:
         self.xs[0] = x
         if self.wgrad_nn:
             # the NN weight-gradient layout's transposed copies of the step's inputs (every other layer's come out of
-            # the producing GEMM epilogues): layer 0's xᵀ and the top layer's dyᵀ
+            # the producing GEMM epilogues): layer 0's xᵀ and the top layer's dyᵀ.  Only weight-gradient GEMMs read
+            # them, so with a weight-gradient stream they are made there, off the forward's critical path (the stream
+            # is joined at the end of every step, and x / dy are not rewritten before the next step)
             from ..ops.gemm import transpose_bf16
 
-            transpose_bf16(x, self.xT[0])
-            transpose_bf16(dy, self.dyT_top)
+            side = self.wg_stream if (self.wg_stream is not None and _TRANSPOSE_ON_SIDE) else None
+            if side is not None:
+                side.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+                if self.wgrad_nn_w2:
+                    transpose_bf16(dy, self.dyT_top)
+                transpose_bf16(x, self.xT[0])
 
         # ---------------- forward ----------------
         mark = self._mark("forward")
@@ -1161,7 +1179,7 @@ class FFNTrainer:
             # optimizer runs, so the reference's re-gather of L-2 (:245) is skipped when still resident
             self._fsdp_gather(L - 2)
         g = dy
-        gT = self.dyT_top if self.wgrad_nn else None    # gᵀ: the NN weight-gradient layout's dW2 operand
+        gT = self.dyT_top if self.wgrad_nn_w2 else None    # gᵀ: the NN weight-gradient layout's dW2 operand
         for l in reversed(range(L)):
             if self.fsdp:
                 if l < L - 1:
@@ -1214,7 +1232,8 @@ class FFNTrainer:
             else:
                 if not keep:
                     recompute_fwd1(self.xs[l], w1, act, gated, a, h, mask=self._mask(l))
-                nn = NNWgrad(self.xT[l], gT, self.dxTb[l % 2] if need_dx else None) if self.wgrad_nn else None
+                nn = (NNWgrad(self.xT[l], gT, self.dxTb[l % 2] if need_dx and self.wgrad_nn_w2 else None)
+                      if self.wgrad_nn else None)
                 dx = layer_bwd(g, self.xs[l], w1, w2, act, gated, a, h, gw1, gw2, self.da,
                                self.dxb[l % 2] if need_dx else None, hooks, mask=self._mask(l),
                                dx_first=self.tp_comm and cfg.tp_overlap, pair_wgrads=self.pair_wgrads, nn=nn)

@@ -111,5 +111,117 @@ def main():
             json.dump({"checks": checks, "median_us": med}, f, indent=1)
 
 
+def operand_order():
+    """Same product, same operands, the two MFMA operand orders: the plain store (B fragment first, lanes hold 4
+    consecutive columns) vs ``out_t`` (A fragment first, lanes hold 4 consecutive rows, output written transposed), for
+    the three layouts on flagship shapes."""
+    g = torch.Generator().manual_seed(1)
+    bf = torch.bfloat16
+    T, D, F = 8192, 4096, 16384
+
+    def rnd(*shape):
+        return torch.randn(*shape, generator=g).to(bf).cuda()
+
+    a, w2, da, w1, dy = rnd(T, F), rnd(D, F), rnd(T, F), rnd(F, D), rnd(T, D)
+    dyT = dy.t().contiguous()
+    cases = {  # name: (A, B, layout, out shape)
+        "nt y=a.W2t": (a, w2, "nt", (T, D)),
+        "nn dx=da.W1": (da, w1, "nn", (T, D)),
+        "nn dW2=dyT.a": (dyT, a, "nn", (D, F)),
+        "tn dW2=dy^T.a": (dy, a, "tn", (D, F)),
+    }
+    for name, (A, B, lay, (M, N)) in cases.items():
+        o, ot = torch.empty(M, N, dtype=bf, device="cuda"), torch.empty(N, M, dtype=bf, device="cuda")
+        gemm(A, B, lay, out=o)
+        gemm(A, B, lay, out=ot, out_t=True)
+        same = bool(torch.equal(o, ot.t()))
+        r0, r1 = [], []
+        for _ in range(5):
+            r0.append(timeit(lambda: gemm(A, B, lay, out=o), 10))
+            r1.append(timeit(lambda: gemm(A, B, lay, out=ot, out_t=True), 10))
+        print(f"{name:16s} B-first {statistics.median(r0):7.1f} us  A-first(out_t) {statistics.median(r1):7.1f} us  "
+              f"bitwise {same}", flush=True)
+
+
+
+
+def epilogue_shapes():
+    """Fused split-master SGD epilogue cost by output shape and map: the same NN product (K = 8192) updating a
+    [4096, 16384] or a [16384, 4096] master, natural (lanes along the row) or transposed (``out_t``); cost = fused minus
+    the same GEMM's plain bf16 store."""
+    g = torch.Generator().manual_seed(2)
+    bf = torch.bfloat16
+    K = 8192
+
+    def rnd(*shape, s=1.0):
+        return (torch.randn(*shape, generator=g) * s).to(bf).cuda()
+
+    for (M, N) in ((4096, 16384), (16384, 4096)):
+        A, B = rnd(M, K), rnd(K, N)
+        for out_t in (False, True):
+            shp = (N, M) if out_t else (M, N)
+            hi, lo = split_master((torch.randn(*shp, generator=g) * 0.02).cuda())
+            st = torch.empty(*shp, dtype=bf, device="cuda")
+            r0, r1 = [], []
+            for _ in range(5):
+                r0.append(timeit(lambda: gemm(A, B, "nn", out=st, out_t=out_t), 10))
+                r1.append(timeit(lambda: gemm(A, B, "nn", out=lo, epi="sgd_split", lr=1e-9, aux_out=hi, out_t=out_t),
+                                 10))
+            s0, s1 = statistics.median(r0), statistics.median(r1)
+            print(f"NN M={M:5d} N={N:5d} {'out_t' if out_t else 'natural'}: master {shp}, store {s0:7.1f} us, "
+                  f"fused SGD {s1:7.1f} us, epilogue {s1 - s0:6.1f} us", flush=True)
+
+
+
+
+def epilogue_raster():
+    """The natural [4096, 16384] fused-SGD weight gradient (dW2's master) by raster band height group_m."""
+    g = torch.Generator().manual_seed(3)
+    bf = torch.bfloat16
+    M, N, K = 4096, 16384, 8192
+    A = torch.randn(M, K, generator=g).to(bf).cuda()
+    B = torch.randn(K, N, generator=g).to(bf).cuda()
+    hi, lo = split_master((torch.randn(M, N, generator=g) * 0.02).cuda())
+    st = torch.empty(M, N, dtype=bf, device="cuda")
+    for gm in (1, 2, 4, 8, 16):
+        r0, r1 = [], []
+        for _ in range(5):
+            r0.append(timeit(lambda: gemm(A, B, "nn", out=st, group_m=gm), 10))
+            r1.append(timeit(lambda: gemm(A, B, "nn", out=lo, epi="sgd_split", lr=1e-9, aux_out=hi, group_m=gm), 10))
+        s0, s1 = statistics.median(r0), statistics.median(r1)
+        print(f"group_m {gm:2d}: store {s0:7.1f} us, fused SGD {s1:7.1f} us, epilogue {s1 - s0:6.1f} us", flush=True)
+
+
+
+
+def epilogue_pitch():
+    """The natural [4096, 16384] fused-SGD weight gradient with the master rows padded (row pitch 16384 + pad
+    elements): does the 32-KiB power-of-two row pitch cost the epilogue's HBM writes?"""
+    g = torch.Generator().manual_seed(4)
+    bf = torch.bfloat16
+    M, N, K = 4096, 16384, 8192
+    A = torch.randn(M, K, generator=g).to(bf).cuda()
+    B = torch.randn(K, N, generator=g).to(bf).cuda()
+    for pad in (0, 64, 128, 256, 2048):
+        hi_f, lo_f = split_master((torch.randn(M, N + pad, generator=g) * 0.02).cuda())
+        hi, lo = hi_f[:, :N], lo_f[:, :N]
+        st = torch.empty(M, N + pad, dtype=bf, device="cuda")[:, :N]
+        r0, r1 = [], []
+        for _ in range(5):
+            r0.append(timeit(lambda: gemm(A, B, "nn", out=st), 10))
+            r1.append(timeit(lambda: gemm(A, B, "nn", out=lo, epi="sgd_split", lr=1e-9, aux_out=hi), 10))
+        s0, s1 = statistics.median(r0), statistics.median(r1)
+        print(f"pitch {N + pad:6d}: store {s0:7.1f} us, fused SGD {s1:7.1f} us, epilogue {s1 - s0:6.1f} us", flush=True)
+
+
 if __name__ == "__main__":
-    main()
+    if "--operand_order" in sys.argv:   # python scripts/bench_nn_wgrad.py --operand_order
+        operand_order()
+    elif "--epilogue_pitch" in sys.argv:
+        epilogue_pitch()
+    elif "--epilogue_raster" in sys.argv:
+        epilogue_raster()
+    elif "--epilogue_shapes" in sys.argv:
+        epilogue_shapes()
+    else:
+        main()

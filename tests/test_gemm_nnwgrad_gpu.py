@@ -105,30 +105,32 @@ def test_transposed_outputs_reject_bad_shapes():
     with pytest.raises(ValueError):
         gemm(b.t().contiguous(), a[:192], "nn", out_t=True)
     with pytest.raises(ValueError):
-        gemm(a, a, "tn", out_t=True)                     # transposed outputs: NN only
+        gemm(a, a, "tn", out_t=True, epi="sgd_split")    # transposed fused optimizer: NN only
 
 
 @pytest.mark.parametrize("variant", ["fused_serial", "fused_wgrad_stream", "grads_fp32", "grads_bf16"])
-def test_engine_nn_wgrad_layout_bitwise_tn(variant):
+def test_engine_nn_wgrad_layout_bitwise_tn(variant, monkeypatch):
     """Three layers, three steps: the engine's NN weight-gradient layout (transposed copies from the fwd-2 / dx
     epilogues and the step-start transposes) leaves masters bitwise equal to the TN layout's -- fused split-master SGD
-    on the serial backward and on the concurrent weight-gradient stream, and stored (fp32 / bf16) gradients."""
+    on the serial backward and on the concurrent weight-gradient stream (off by default with NN, kept for A/B runs),
+    and stored (fp32 / bf16) gradients."""
     from dllm.models.ffn import init_ffn_params_device
     from dllm.parallel.engine import FFNTrainer
     from dllm.parallel.mesh import Mesh
     from dllm.utils.config import ModelConfig, TrainConfig
     from dllm.utils.data import DeviceMockData
 
+    monkeypatch.setenv("DLLM_NN_CONCURRENT", "1")   # keep the (A/B-only) concurrent NN path covered
     dev = torch.device("cuda", 0)
     m = ModelConfig(model_size=2048, ffn_dim=8192, layers=3, act="relu")   # tile grids too big for the pair
     out = {}
-    for layout in ("tn", "nn"):
+    for layout in ("tn", "nn", "nn_w1"):
         cfg = TrainConfig(model=m, batch_size=1, seq_len=1024, dtype="bf16",
                           grad_dtype="bf16" if variant == "grads_bf16" else "fp32", optimizer="sgd", lr=1e-3,
                           wgrad_layout=layout, wgrad_stream=variant == "fused_wgrad_stream",
                           fused_optimizer=variant.startswith("fused"))
         eng = FFNTrainer(cfg, Mesh(), dev)
-        assert eng.wgrad_nn == (layout == "nn")
+        assert eng.wgrad_nn == (layout != "tn") and eng.wgrad_nn_w2 == (layout == "nn")
         assert (eng.wg_stream is not None) == (variant == "fused_wgrad_stream")
         eng.load_full_params(init_ffn_params_device(m.D, m.F, m.layers, 7, dev))
         data = DeviceMockData(cfg.tokens, m.D, torch.bfloat16, dev)
@@ -139,6 +141,7 @@ def test_engine_nn_wgrad_layout_bitwise_tn(variant):
         torch.cuda.synchronize()
         out[layout] = (eng.master.clone(), ys)
     bits = lambda t: t.view(torch.int16 if t.dtype == BF else torch.int32)   # noqa: E731 (NaN-safe bitwise)
-    assert all(torch.equal(bits(a), bits(b)) for a, b in zip(out["tn"][1], out["nn"][1]))
-    assert torch.equal(bits(out["tn"][0]), bits(out["nn"][0]))
+    for layout in ("nn", "nn_w1"):
+        assert all(torch.equal(bits(a), bits(b)) for a, b in zip(out["tn"][1], out[layout][1])), layout
+        assert torch.equal(bits(out["tn"][0]), bits(out[layout][0])), layout
     assert torch.isfinite(out["nn"][0]).all()
