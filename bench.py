@@ -180,7 +180,7 @@ def parse(argv=None):
                         "update into the wgrad GEMM epilogue)")
     p.add_argument("--phases", action="store_true",
                    help="also report per-phase GPU time (forward / backward / optimizer tail) from HIP events")
-    p.add_argument("--wgrad_layout", choices=["auto", "tn", "nn", "nn_w1"], default="auto",
+    p.add_argument("--wgrad_layout", choices=["auto", "tn", "nn", "nn_w1", "nn_w2t"], default="auto",
                    help="weight-gradient GEMM layout: nn = transposed xᵀ / dyᵀ copies written by the producing "
                         "epilogues, both weight gradients as NN GEMMs with a K-contiguous A (models/ffn.NNWgrad); "
                         "auto = nn wherever the engine supports it")

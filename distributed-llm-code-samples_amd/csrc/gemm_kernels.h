@@ -2131,7 +2131,10 @@ constexpr bool persistent_kernel() {
   if constexpr (E == EPI_STORE_DT || E == EPI_STORE_T || E == EPI_SGDS_T) return true;
   if constexpr (L == L_NN && E == EPI_SGDS) return true;   // the NN weight-gradient layout (dispatch_x)
   // gated (SwiGLU) stacks: the GLU forward / DGLU dgrad with a compile-time activation (round 3)
-  if constexpr (L == L_NT) return bf && ((E == EPI_ACT && ACT == ACT_RELU) || E == EPI_STORE || (E == EPI_GLU && ACT >= 0));
+  // NT dgrad with the ReLU mask: W2 stored as W2ᵀ (the nn_w2t weight-gradient mode, parallel/engine.py)
+  if constexpr (L == L_NT)
+    return bf && ((E == EPI_ACT && ACT == ACT_RELU) || E == EPI_STORE || (E == EPI_GLU && ACT >= 0) ||
+                  (E == EPI_DACT && ACT == ACT_RELU));
   if constexpr (L == L_NN) return bf && ((E == EPI_DACT && ACT == ACT_RELU) || E == EPI_STORE || (E == EPI_DGLU && ACT >= 0));
   return E == EPI_STORE || E == EPI_SGD || E == EPI_SGDS;
 }
@@ -2182,7 +2185,7 @@ static void launch_8ph_act(const GemmArgs& a0, int nb0, hipStream_t s) {
 template <int L, int E, typename OutT, int NPH>
 static void launch_8ph_stagger(const GemmArgs& a, int nb, hipStream_t s) {
   constexpr bool fwd = L == L_NT && (E == EPI_ACT || E == EPI_GLU);
-  constexpr bool bwd = L == L_NN && (E == EPI_DACT || E == EPI_DGLU);
+  constexpr bool bwd = (L == L_NN && (E == EPI_DACT || E == EPI_DGLU)) || (L == L_NT && E == EPI_DACT && NPH == 8);
   if constexpr ((fwd || bwd) && std::is_same<OutT, uint16_t>::value) {
     switch (a.act) {
       case ACT_RELU: launch_8ph_act<L, E, OutT, ACT_RELU, NPH>(a, nb, s); return;

@@ -96,18 +96,20 @@ def needs_preact(act: str, gated: bool) -> bool:
 
 def layer_fwd(x: torch.Tensor, w1: torch.Tensor, w2: torch.Tensor, act: str, gated: bool,
               a_out: torch.Tensor, h_out: torch.Tensor | None, y_out: torch.Tensor,
-              before_fwd2=None, mask: torch.Tensor | None = None, y_t: torch.Tensor | None = None) -> torch.Tensor:
+              before_fwd2=None, mask: torch.Tensor | None = None, y_t: torch.Tensor | None = None,
+              w2t: bool = False) -> torch.Tensor:
     """y = act(x·W1ᵀ)·W2ᵀ  (gated: (act(x·W1ᵀ)⊙x·W3ᵀ)·W2ᵀ with ``w1`` = interleaved W13).
     ``before_fwd2()`` runs between the two GEMMs (e.g. waiting for W2's all-gather).  ``mask`` (ReLU):
     the first GEMM also writes the activation-gradient bitmask the backward's dgrad reads.  ``y_t`` (NN weight-gradient
-    layout): the second GEMM's epilogue also writes yᵀ [D, T], the next layer's dW1 operand."""
+    layout): the second GEMM's epilogue also writes yᵀ [D, T], the next layer's dW1 operand.  ``w2t``: ``w2`` is the
+    stored W2ᵀ [F, D] (y = a·W2ᵀ then runs NN)."""
     if gated:
         gemm(x, w1, "nt", out=a_out, epi="glu", act=act, aux_out=h_out)
     else:
         gemm(x, w1, "nt", out=a_out, epi="act", act=act, aux_out=h_out, mask=mask)
     if before_fwd2 is not None:
         before_fwd2()
-    gemm(a_out, w2, "nt", out=y_out, aux_t=y_t)
+    gemm(a_out, w2, "nn" if w2t else "nt", out=y_out, aux_t=y_t)
     return y_out
 
 
@@ -124,11 +126,14 @@ class NNWgrad(NamedTuple):
     x_t: torch.Tensor
     dy_t: torch.Tensor | None
     dx_t: torch.Tensor | None
+    w2t: bool = False    # W2 stored as W2ᵀ [F, D] (nn_w2t): dW2ᵀ written through the transposed map, dgrad NT
 
 
 def wgrad_w2(dy: torch.Tensor, a: torch.Tensor, kw2: dict, nn: NNWgrad | None) -> None:
     if nn is None or nn.dy_t is None:
         gemm(dy, a, "tn", **kw2)                                      # dW2 = dyᵀ·a        [D, F]
+    elif nn.w2t:
+        gemm(nn.dy_t, a, "nn", out_t=True, **kw2)                     # dW2 = (dyᵀ)·a      -> W2ᵀ [F, D]
     else:
         gemm(nn.dy_t, a, "nn", **kw2)                                 # dW2 = (dyᵀ)·a      [D, F]
 
@@ -164,10 +169,12 @@ def layer_bwd(dy: torch.Tensor, x: torch.Tensor, w1: torch.Tensor, w2: torch.Ten
 
     ``nn`` (``NNWgrad``): the weight gradients in the NN layout; dx's epilogue also writes dxᵀ into ``nn.dx_t``.
     """
+    w2_layout = "nt" if nn is not None and nn.w2t else "nn"           # w2t: w2 is the stored W2ᵀ [F, D]
     if gated:
+        assert w2_layout == "nn", "gated layers keep W2 row-major"
         gemm(dy, w2, "nn", out=da_buf, epi="dglu", act=act, aux=h)    # [dg|du] interleaved [T, 2F]
     else:
-        gemm(dy, w2, "nn", out=da_buf, epi="dact", act=act, aux=h if h is not None else a, mask=mask)
+        gemm(dy, w2, w2_layout, out=da_buf, epi="dact", act=act, aux=h if h is not None else a, mask=mask)
     kw1 = gw1 if isinstance(gw1, dict) else {"out": gw1}
     kw2 = gw2 if isinstance(gw2, dict) else {"out": gw2}
     if pair_wgrads:

@@ -203,8 +203,47 @@ class FFNTrainer:
             if self.tp_car is not None:
                 mesh.groups["tp_car"] = self.tp_car
 
+        # ---- optimizer / weight-gradient modes (they decide the parameter layout below) ----------------
+        # no gradient collective (single device / pure TP): the optimizer runs inside the wgrad GEMMs and
+        # no flat gradient buffer exists at all
+        no_coll = not (self.ddp or self.fsdp or self.zero)
+        # side-stream optimizer: wgrad GEMMs store the gradient, a low-occupancy SGD kernel on its own
+        # stream updates the weight while the next GEMMs run; the forward waits per weight
+        # (SGD only: a side-stream AdamW on the split master was measured 63 % slower on config 5 and removed, round 5,
+        # profiles/r5/adamw_fused_vs_side_r5.txt)
+        self.side_opt = (no_coll and cfg.side_optimizer > 0 and cfg.optimizer == "sgd" and dev.type == "cuda")
+        # Split master (bf16 SGD): the fp32 master is the bf16 working copy (hi) plus an int16 residual plane (lo),
+        # bitwise the same fp32 values (ops/master.py).  4 B/param of weight state instead of 6 B, and every update
+        # (fused wgrad epilogue or flat kernel) reads 4 B and writes 4 B per parameter instead of 4 B + 6 B.
+        self.split = cfg.master == "split" and self.cd == torch.bfloat16 and not self.side_opt
+        if cfg.master not in ("split", "fp32"):
+            raise ValueError(f"unknown master format {cfg.master!r}")
+        self.fused_opt = cfg.fused_optimizer and no_coll and not self.side_opt
+        # grouped weight-gradient pair (small tile grids: the MP / TP8 shard's dW2 [D, F/8] and dW1 [F/8, D] would each
+        # run split-K plus a reduction pass): both in one launch of whole tiles, after dx (models/ffn.layer_bwd).  It
+        # replaces the weight-gradient stream there: two part-empty grids have no tail worth filling
+        self.pair_wgrads = False
+        if dev.type == "cuda" and not self.tmode:
+            from ..ops.gemm import pair_supported
+
+            self.pair_wgrads = pair_supported(((D, self.F_loc, T), (self.R1, D, T)), self.cd)
+        # NN weight-gradient layout (models/ffn.NNWgrad; buffers below).  It runs the backward serially: with the
+        # concurrent weight-gradient stream it measured 0.35-0.45 ms per step slower than serial (3 interleaved pairs,
+        # profiles/r5/nn_wgrad_step_ab_r5.txt), serial NN 0.1-0.4 ms faster than the TN layout on the stream
+        # (DLLM_NN_CONCURRENT=1 keeps the stream for A/B runs).  Modes: nn_w1 = dW1 only; nn = dW2 as well, W2 row-major
+        # (dW2's master rows 32 KiB apart); nn_w2t (auto) = dW2 as well with W2 stored transposed (W2ᵀ [F, D], the
+        # transposed-activation mode's storage): dW2 then writes through the transposed map, fwd-2 runs NN and the
+        # dgrad NT.  Flagship, serial, 3 interleaved triplets: tn 29.33-29.53, nn_w1 29.09-29.30, nn_w2t 28.26-28.30 ms
+        # (profiles/r5/nn_wgrad_step_ab_r5.txt)
+        mode = "nn_w2t" if cfg.wgrad_layout == "auto" else cfg.wgrad_layout
+        self.wgrad_nn = self._wgrad_nn_supported() and mode in ("nn", "nn_w1", "nn_w2t")   # dW1 as NN (out_t)
+        self.wgrad_nn_w2 = self.wgrad_nn and mode in ("nn", "nn_w2t")                        # dW2 as NN too
+        self.w2t_nn = self.wgrad_nn and mode == "nn_w2t" and not self.gated
+        # W2 stored as W2ᵀ [F_loc, D]: the transposed-activation TP layout, or the nn_w2t weight-gradient mode
+        self.w2t = self.tmode or self.w2t_nn
+
         # ---- flat owned parameter layout (completion order) ------------------------------------
-        full = {"w2": (self.F_loc, D) if self.tmode else (D, self.F_loc), "w1": (self.R1, D)}
+        full = {"w2": (self.F_loc, D) if self.w2t else (D, self.F_loc), "w1": (self.R1, D)}
         self.entries: list[Entry] = []
         off = 0
         # ZeRO shards every bucket evenly over dp ranks: keep every entry a multiple of dp*ALIGN
@@ -251,25 +290,12 @@ class FFNTrainer:
         # ---- flat state ----------------------------------------------------------------------------
         # no gradient collective (single device / pure TP): the optimizer runs inside the wgrad GEMMs and
         # no flat gradient buffer exists at all
-        no_coll = not (self.ddp or self.fsdp or self.zero)
-        # side-stream optimizer: wgrad GEMMs store the gradient, a low-occupancy SGD kernel on its own
-        # stream updates the weight while the next GEMMs run; the forward waits per weight
-        # (SGD only: a side-stream AdamW on the split master was measured 63 % slower on config 5 and removed, round 5,
-        # profiles/r5/adamw_fused_vs_side_r5.txt)
-        self.side_opt = (no_coll and cfg.side_optimizer > 0 and cfg.optimizer == "sgd" and dev.type == "cuda")
-        # Split master (bf16 SGD): the fp32 master is the bf16 working copy (hi) plus an int16 residual plane (lo),
-        # bitwise the same fp32 values (ops/master.py).  4 B/param of weight state instead of 6 B, and every update
-        # (fused wgrad epilogue or flat kernel) reads 4 B and writes 4 B per parameter instead of 4 B + 6 B.
         nmaster = self.shard_total if self.zero else self.total
-        self.split = cfg.master == "split" and self.cd == torch.bfloat16 and not self.side_opt
-        if cfg.master not in ("split", "fp32"):
-            raise ValueError(f"unknown master format {cfg.master!r}")
         self._master = None if self.split else torch.zeros(nmaster, dtype=torch.float32, device=dev)
         self.master_lo = torch.zeros(nmaster, dtype=torch.int16, device=dev) if self.split else None
         self._master_stage = None  # split: the fp32 master last materialised by `master` (written back by refresh_copy)
         self.shared_copy = self.cd == torch.float32 and not self.zero
         self.copy = self._master if self.shared_copy else torch.zeros(self.total, dtype=self.cd, device=dev)
-        self.fused_opt = cfg.fused_optimizer and no_coll and not self.side_opt
         self.grads = torch.zeros(0 if self.fused_opt else self.total, dtype=self.gd, device=dev)
         if self.side_opt:
             self.opt_stream_side = self._side_stream("side_opt")
@@ -365,18 +391,7 @@ class FFNTrainer:
         # grouped weight-gradient pair (small tile grids: the MP / TP8 shard's dW2 [D, F/8] and dW1 [F/8, D] would each
         # run split-K plus a reduction pass): both in one launch of whole tiles, after dx (models/ffn.layer_bwd).  It
         # replaces the weight-gradient stream there: two part-empty grids have no tail worth filling
-        self.pair_wgrads = False
-        if dev.type == "cuda" and not self.tmode:
-            from ..ops.gemm import pair_supported
-
-            self.pair_wgrads = pair_supported(((D, self.F_loc, T), (self.R1, D, T)), self.cd)
-        # NN weight-gradient layout (models/ffn.NNWgrad; buffers below).  It runs the backward serially: with the
-        # concurrent weight-gradient stream it measured 0.35-0.45 ms per step slower than serial (3 interleaved pairs,
-        # profiles/r5/nn_wgrad_step_ab_r5.txt), serial NN 0.1-0.4 ms faster than the TN layout on the stream
-        # (DLLM_NN_CONCURRENT=1 keeps the stream for A/B runs)
-        mode = "nn_w1" if cfg.wgrad_layout == "auto" else cfg.wgrad_layout
-        self.wgrad_nn = self._wgrad_nn_supported() and mode in ("nn", "nn_w1")   # dW1 as NN (out_t)
-        self.wgrad_nn_w2 = self.wgrad_nn and mode == "nn"                          # dW2 as NN too
+        # (self.pair_wgrads and the NN weight-gradient mode are decided before the parameter layout, above)
         self.wg_stream = None
         wg_tiles = -(-self.R1 // 256) * -(-D // 256)
         ncu = torch.cuda.get_device_properties(dev).multi_processor_count if dev.type == "cuda" else 256
@@ -431,7 +446,7 @@ class FFNTrainer:
         plain row-major layer (no TP / SP / FSDP / transposed-activation mode / recompute / grouped pair / TP chunks),
         256x256 8-phase shapes, and a fused optimizer only as SGD on split masters (stored gradients: any)."""
         cfg = self.cfg
-        if cfg.wgrad_layout not in ("auto", "tn", "nn", "nn_w1"):
+        if cfg.wgrad_layout not in ("auto", "tn", "nn", "nn_w1", "nn_w2t"):
             raise ValueError(f"unknown wgrad_layout {cfg.wgrad_layout!r}")
         if cfg.wgrad_layout == "tn":
             return False
@@ -441,7 +456,7 @@ class FFNTrainer:
         why = []
         if self.device.type != "cuda" or self.cd != torch.bfloat16:
             why.append("GPU bf16 only")
-        if self.tp_comm or self.sp or self.fsdp or self.tmode or self.pair_wgrads or self.tp_chunks > 1:
+        if self.tp_comm or self.sp or self.fsdp or self.tmode or self.pair_wgrads:
             why.append("row-major data-parallel / single-device layers only")
         if cfg.recompute != "none":
             why.append("kept activations only")
@@ -449,7 +464,7 @@ class FFNTrainer:
             why.append("fused optimizer: SGD on split masters only")
         if not (nn_wgrad_supported(D, self.F_loc, T) and nn_wgrad_supported(D, self.R1, T) and T % 64 == 0):
             why.append(f"shapes (D={D}, F={self.F_loc}, T={T}) off the 256x256 8-phase tiles")
-        if why and cfg.wgrad_layout in ("nn", "nn_w1"):
+        if why and cfg.wgrad_layout in ("nn", "nn_w1", "nn_w2t"):
             raise ValueError(f"wgrad_layout {cfg.wgrad_layout}: " + "; ".join(why))
         return not why
 
@@ -463,7 +478,7 @@ class FFNTrainer:
         """The stored 2-D tensor of ``e`` in the logical [out, in] orientation (a transposed view of W2ᵀ in the
         transposed-activation layout; checkpoints read and write through it)."""
         v = self._view(flat, e)
-        return v.t() if (self.tmode and e.name == "w2") else v
+        return v.t() if (self.w2t and e.name == "w2") else v
 
     @property
     def master(self) -> torch.Tensor:
@@ -564,13 +579,14 @@ class FFNTrainer:
         if self.gated:   # [dg|du] interleaved [T, 2F] (as layer_bwd)
             gemm(g, w2, "nn", out=da, epi="dglu", act=act, aux=h)
         else:
-            gemm(g, w2, "nn", out=da, epi="dact", act=act, aux=h if h is not None else a, mask=self._mask(l))
+            gemm(g, w2, "nt" if self.w2t_nn else "nn", out=da, epi="dact", act=act, aux=h if h is not None else a,
+                 mask=self._mask(l))
         e_da = torch.cuda.Event()
         e_da.record(main)
         side.wait_event(e_da)
         j = l % 3
         if self.wgrad_nn:
-            nn = NNWgrad(self.xT[l], gT, self.dxTb[j] if need_dx and self.wgrad_nn_w2 else None)
+            nn = NNWgrad(self.xT[l], gT, self.dxTb[j] if need_dx and self.wgrad_nn_w2 else None, self.w2t_nn)
         if need_dx:
             with torch.cuda.stream(side):
                 wgrad_w2(g, a, kw2, nn)                                   # dW2 = dyᵀ·a
@@ -617,7 +633,7 @@ class FFNTrainer:
         if self.gated:
             w1 = interleave_w13(w1, p["w3"][r * Fl:(r + 1) * Fl])
         w2 = p["w2"][:, r * Fl:(r + 1) * Fl]
-        if self.tmode:
+        if self.w2t:
             w2 = w2.t().contiguous()   # stored as W2ᵀ [F_loc, D]
         return {"w1": w1, "w2": w2}
 
@@ -780,7 +796,7 @@ class FFNTrainer:
             for name in ("w1", "w2"):
                 e = self.entry[(l, name)]
                 mv = self.master_slice(e.offset, e.offset + e.numel).view(e.shape) if per_entry else self._view(src, e)
-                if self.tmode and name == "w2":
+                if self.w2t and name == "w2":
                     mv = mv.t()   # logical [D, F_loc] from the stored W2ᵀ
                 if self.fsdp:
                     full = torch.empty(self.entry[(l, name)].full_shape, dtype=torch.float32, device=self.device)
@@ -1146,7 +1162,8 @@ class FFNTrainer:
                     layer_fwd_t(self.xs[l], w1, w2, act, a, h, self.xs[l + 1], before_fwd2=before2, mask=self._mask(l))
                 else:
                     layer_fwd(self.xs[l], w1, w2, act, gated, a, h, self.xs[l + 1], before_fwd2=before2,
-                              mask=self._mask(l), y_t=self.xT[l + 1] if self.wgrad_nn and l + 1 < L else None)
+                              mask=self._mask(l), y_t=self.xT[l + 1] if self.wgrad_nn and l + 1 < L else None,
+                              w2t=self.w2t_nn)
                 if self.tp_comm:
                     last = l == L - 1
                     if self.tp_car is not None:
@@ -1232,8 +1249,8 @@ class FFNTrainer:
             else:
                 if not keep:
                     recompute_fwd1(self.xs[l], w1, act, gated, a, h, mask=self._mask(l))
-                nn = (NNWgrad(self.xT[l], gT, self.dxTb[l % 2] if need_dx and self.wgrad_nn_w2 else None)
-                      if self.wgrad_nn else None)
+                nn = (NNWgrad(self.xT[l], gT, self.dxTb[l % 2] if need_dx and self.wgrad_nn_w2 else None,
+                              self.w2t_nn) if self.wgrad_nn else None)
                 dx = layer_bwd(g, self.xs[l], w1, w2, act, gated, a, h, gw1, gw2, self.da,
                                self.dxb[l % 2] if need_dx else None, hooks, mask=self._mask(l),
                                dx_first=self.tp_comm and cfg.tp_overlap, pair_wgrads=self.pair_wgrads, nn=nn)

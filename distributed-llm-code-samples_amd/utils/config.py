@@ -73,9 +73,10 @@ class TrainConfig:
     # every F-sized GEMM dimension runs on 224-row tiles that fill the chip (models/ffn.layer_fwd_t / layer_bwd_t)
     tp_transposed: bool = True
     # weight-gradient GEMM layout: "tn" (dW = dyᵀ·a, daᵀ·x: both operands through transposed LDS reads), "nn"
-    # (transposed copies xᵀ / dyᵀ [D, T] from the producing epilogues; models/ffn.NNWgrad) or "nn_w1" (dW1 only: xᵀ
-    # copies; dW2 stays TN); "auto" = nn_w1 where the engine supports it (GPU, bf16, 256x256 8-phase shapes, no TP /
-    # SP / FSDP / recompute, SGD on split masters or stored gradients)
+    # (transposed copies xᵀ / dyᵀ [D, T] from the producing epilogues; models/ffn.NNWgrad), "nn_w1" (dW1 only: xᵀ
+    # copies; dW2 stays TN) or "nn_w2t" (nn with W2 stored as W2ᵀ [F, D]: both weight gradients written through the
+    # transposed map); "auto" = nn_w2t where the engine supports it (GPU, bf16, 256x256 8-phase shapes, no TP / SP /
+    # FSDP / recompute, SGD on split masters or stored gradients; gated stacks keep W2 row-major)
     wgrad_layout: str = "auto"
     wgrad_stream: bool = False       # single device, fused optimizer: weight-gradient GEMMs on a second
                                      # stream, concurrent with the dgrad chain (CUs shared; epilogues overlap)
@@ -143,7 +144,7 @@ def add_extended_args(p: argparse.ArgumentParser) -> None:
                    help="communicator implementation for the role groups (native = C++ RCCL layer)")
     p.add_argument("--tp_allreduce", choices=["rccl", "custom", "auto"], default="rccl",
                    help="TP activation all-reduce: RCCL or the custom two-shot xGMI peer all-reduce")
-    p.add_argument("--wgrad_layout", choices=["auto", "tn", "nn", "nn_w1"], default="auto",
+    p.add_argument("--wgrad_layout", choices=["auto", "tn", "nn", "nn_w1", "nn_w2t"], default="auto",
                    help="weight-gradient GEMM layout (nn: transposed xᵀ / dyᵀ copies from the producing epilogues)")
     p.add_argument("--nprocs", type=int, default=0, help="ranks to spawn (0 = all visible GPUs)")
     p.add_argument("--dp", type=int, default=0)

@@ -124,13 +124,14 @@ def test_engine_nn_wgrad_layout_bitwise_tn(variant, monkeypatch):
     dev = torch.device("cuda", 0)
     m = ModelConfig(model_size=2048, ffn_dim=8192, layers=3, act="relu")   # tile grids too big for the pair
     out = {}
-    for layout in ("tn", "nn", "nn_w1"):
+    for layout in ("tn", "nn", "nn_w1", "nn_w2t"):
         cfg = TrainConfig(model=m, batch_size=1, seq_len=1024, dtype="bf16",
                           grad_dtype="bf16" if variant == "grads_bf16" else "fp32", optimizer="sgd", lr=1e-3,
                           wgrad_layout=layout, wgrad_stream=variant == "fused_wgrad_stream",
                           fused_optimizer=variant.startswith("fused"))
         eng = FFNTrainer(cfg, Mesh(), dev)
-        assert eng.wgrad_nn == (layout != "tn") and eng.wgrad_nn_w2 == (layout == "nn")
+        assert eng.wgrad_nn == (layout != "tn") and eng.wgrad_nn_w2 == (layout in ("nn", "nn_w2t"))
+        assert eng.w2t == (layout == "nn_w2t")
         assert (eng.wg_stream is not None) == (variant == "fused_wgrad_stream")
         eng.load_full_params(init_ffn_params_device(m.D, m.F, m.layers, 7, dev))
         data = DeviceMockData(cfg.tokens, m.D, torch.bfloat16, dev)
@@ -139,9 +140,11 @@ def test_engine_nn_wgrad_layout_bitwise_tn(variant, monkeypatch):
             x, dy = data.fill(i)
             ys.append(eng.train_step(x, dy).clone())
         torch.cuda.synchronize()
-        out[layout] = (eng.master.clone(), ys)
+        # logical [out, in] parameters (nn_w2t stores W2 as W2ᵀ: the flat master's layout differs)
+        params = torch.cat([t.reshape(-1) for p in eng.local_params() for t in (p["w1"], p["w2"])])
+        out[layout] = (params.clone(), ys)
     bits = lambda t: t.view(torch.int16 if t.dtype == BF else torch.int32)   # noqa: E731 (NaN-safe bitwise)
-    for layout in ("nn", "nn_w1"):
+    for layout in ("nn", "nn_w1", "nn_w2t"):
         assert all(torch.equal(bits(a), bits(b)) for a, b in zip(out["tn"][1], out[layout][1])), layout
         assert torch.equal(bits(out["tn"][0]), bits(out[layout][0])), layout
     assert torch.isfinite(out["nn"][0]).all()
