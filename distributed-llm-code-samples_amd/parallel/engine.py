@@ -450,7 +450,7 @@ class FFNTrainer:
             raise ValueError(f"unknown wgrad_layout {cfg.wgrad_layout!r}")
         if cfg.wgrad_layout == "tn":
             return False
-        from ..ops.gemm import nn_wgrad_supported
+        from ..ops.gemm import _VARIANT, BF16_VARIANTS, choose_ksplit, nn_wgrad_supported
 
         T, D = self.T, self.D
         why = []
@@ -464,6 +464,13 @@ class FFNTrainer:
             why.append("fused optimizer: SGD on split masters only")
         if not (nn_wgrad_supported(D, self.F_loc, T) and nn_wgrad_supported(D, self.R1, T) and T % 64 == 0):
             why.append(f"shapes (D={D}, F={self.F_loc}, T={T}) off the 256x256 8-phase tiles")
+        elif (choose_ksplit(D, self.F_loc, T) > 1 or choose_ksplit(self.R1, D, T) > 1
+              or choose_ksplit(T, D, self.F_loc) > 1):
+            # small tile grids: the TN weight gradients / the fwd-2 and dx stores run split-K, which the transposed
+            # outputs and copies do not (a different summation order: results would stop matching the TN layout's)
+            why.append(f"small tile grids (T={T}, D={D}, F={self.F_loc}) take split-K")
+        if BF16_VARIANTS.get(_VARIANT["name"], 0) not in (0, 3):
+            why.append(f"GEMM variant {_VARIANT['name']}: transposed outputs run on the 8-phase staggered kernels only")
         if why and cfg.wgrad_layout in ("nn", "nn_w1", "nn_w2t"):
             raise ValueError(f"wgrad_layout {cfg.wgrad_layout}: " + "; ".join(why))
         return not why

@@ -25,12 +25,15 @@ def _round_up(n: int, a: int) -> int:
 def plan(D: int, F: int, L: int, tokens: int, dp: int = 1, tp: int = 1, mode: str = "none", gated: bool = False,
          act: str = "relu", dtype: str = "bf16", grad_dtype: str = "bf16", optimizer: str = "sgd",
          recompute: str = "none", relu_mask: bool = True, sequence_parallel: bool = False,
-         align: int = 64, wgrad_stream: bool = False, master: str = "split") -> dict:
+         align: int = 64, wgrad_stream: bool = False, master: str = "split", wgrad_layout: str = "tn") -> dict:
     """Per-rank bytes by buffer (and GiB totals).  ``mode``: none | ddp | zero | fsdp (over ``dp`` ranks).
     ``wgrad_stream``: the concurrent weight-gradient stream (single device, fused optimizer, kept activations, no
     TP) rotates two dgrad and three dx buffers instead of one and two (``FFNTrainer.da_ring`` / ``dxb``).
     ``master``: "split" keeps a bf16 run's fp32 master as the working copy plus an int16 residual plane
-    (``master_residual``, 2 B/param) instead of a separate fp32 buffer (``master_fp32``, 4 B/param)."""
+    (``master_residual``, 2 B/param) instead of a separate fp32 buffer (``master_fp32``, 4 B/param).
+    ``wgrad_layout`` (the engine's resolved mode, ``FFNTrainer.wgrad_nn`` / ``wgrad_nn_w2``): nn_w1 keeps a transposed
+    copy xᵀ [D, T] of every layer input, nn / nn_w2t also dyᵀ copies rotating with the dx buffers plus the top layer's;
+    the NN modes run the backward serially (no weight-gradient stream)."""
     cd = 2 if dtype == "bf16" else 4
     gd = 2 if grad_dtype == "bf16" else 4
     multi = dp > 1
@@ -71,10 +74,13 @@ def plan(D: int, F: int, L: int, tokens: int, dp: int = 1, tp: int = 1, mode: st
     if relu_mask and act == "relu" and not gated and dtype == "bf16":
         b["relu_masks"] = nA * (T // 256) * (F_loc // 256) * 8192
     # the engine runs the stream only while a weight gradient has <= 4 tiles per CU (TrainConfig.wgrad_stream_max_tpc)
-    ws = (wgrad_stream and fused and tp == 1 and keep and not sp
+    nn = wgrad_layout in ("nn_w1", "nn", "nn_w2t")
+    ws = (wgrad_stream and fused and tp == 1 and keep and not sp and not nn
           and -(-R1 // 256) * -(-D // 256) <= 4 * 256)
     b["dgrad_buffer"] = (2 if ws else 1) * T * R1 * cd
     b["dx_buffers"] = (3 if ws else 2) * T * D * cd
+    if nn:
+        b["nn_transposed_copies"] = (L + (3 if wgrad_layout != "nn_w1" else 0)) * D * T * cd
     if sp:
         b["sp_buffers"] = (3 + (L if keep else 0)) * T * D * cd + 2 * Tl * D * cd
     state = sum(v for k, v in b.items() if k in ("master_fp32", "master_residual", "compute_copy", "grads", "adam_moments",

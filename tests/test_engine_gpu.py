@@ -281,7 +281,7 @@ def test_wgrad_stream_bitwise_full_size(variant):
         outs = []
         for ws in (False, True):
             cfg = TrainConfig(model=ModelConfig(D, F, L, "relu", False), batch_size=8, seq_len=1024, dtype="bf16",
-                              grad_dtype="bf16", wgrad_stream=ws)   # the bench's lr: lr 1e-2 overflows
+                              grad_dtype="bf16", wgrad_stream=ws, wgrad_layout="tn")   # the bench's lr: 1e-2 overflows
             eng = FFNTrainer(cfg, Mesh(), torch.device("cuda"))
             assert (eng.wg_stream is not None) == ws and eng.masks is not None
             eng.load_full_params(init_ffn_params_device(D, F, L, 7, torch.device("cuda"), False))
@@ -306,12 +306,21 @@ def test_sizing_plan_matches_wgrad_stream_buffers():
     from dllm.utils.sizing import plan
 
     cfg = TrainConfig(model=ModelConfig(256, 1024, 3), batch_size=2, seq_len=256, dtype="bf16", grad_dtype="bf16",
-                      lr=1e-2, wgrad_stream=True)
+                      lr=1e-2, wgrad_stream=True, wgrad_layout="tn")
     eng = FFNTrainer(cfg, Mesh(), torch.device("cuda"))
     assert eng.wg_stream is not None
     p = plan(256, 1024, 3, 512, dtype="bf16", grad_dtype="bf16", wgrad_stream=True)["bytes"]
     nb = lambda t: t.numel() * t.element_size()  # noqa: E731
     assert p["dgrad_buffer"] == sum(nb(t) for t in eng.da_ring)
+    assert p["dx_buffers"] == sum(nb(t) for t in eng.dxb)
+    # the NN weight-gradient layout (flagship-shaped layer: tile grids large enough for it): serial, transposed copies
+    cfg = TrainConfig(model=ModelConfig(2048, 8192, 2), batch_size=1, seq_len=8192, dtype="bf16", grad_dtype="bf16",
+                      lr=1e-3, wgrad_stream=True, wgrad_layout="nn_w2t")
+    eng = FFNTrainer(cfg, Mesh(), torch.device("cuda"))
+    assert eng.wg_stream is None and eng.w2t
+    p = plan(2048, 8192, 2, 8192, dtype="bf16", grad_dtype="bf16", wgrad_stream=True, wgrad_layout="nn_w2t")["bytes"]
+    copies = list(eng.xT) + list(eng.dxTb) + [eng.dyT_top]
+    assert p["nn_transposed_copies"] == sum(nb(t) for t in copies)
     assert p["dx_buffers"] == sum(nb(t) for t in eng.dxb)
 
 

@@ -129,7 +129,8 @@ from dllm.utils.data import DeviceMockData
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(0)
 m = ModelConfig(model_size=4096, ffn_dim=16384, layers=1, act="relu")     # flagship layer: weight-gradient stream on
-cfg = TrainConfig(model=m, batch_size=1, seq_len=1024, dtype="bf16", grad_dtype="fp32", optimizer="sgd")
+cfg = TrainConfig(model=m, batch_size=1, seq_len=1024, dtype="bf16", grad_dtype="fp32", optimizer="sgd",
+                  wgrad_stream=True, wgrad_layout="tn")   # the TN layout keeps the weight-gradient side stream
 eng = FFNTrainer(cfg, Mesh(), dev)          # no bench.py, no launcher: the engine reserves the queue itself
 eng.load_full_params(init_ffn_params_device(m.D, m.F, m.layers, 1, dev))
 data = DeviceMockData(cfg.tokens, m.D, torch.bfloat16, dev)
