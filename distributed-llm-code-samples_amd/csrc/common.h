@@ -38,9 +38,10 @@ enum Layout : int { L_NT = 0, L_NN = 1, L_TN = 2 };
 //   EPI_STORE_T : EPI_STORE of Cᵀ (beta = 0), same operand order
 //   EPI_STORE_DT: EPI_STORE (beta = 0, bf16) plus a transposed copy Cᵀ [N, M] into aux_out (ldaux), e.g. a layer's
 //                 output y and its yᵀ for the next layer's NN weight gradient
+//   EPI_ADAMS_T : EPI_ADAMS of Cᵀ (moments in the master's transposed layout)
 enum Epi : int { EPI_STORE = 0, EPI_ACT = 1, EPI_DACT = 2, EPI_GLU = 3, EPI_DGLU = 4, EPI_SGD = 5, EPI_ADAM = 6,
-                 EPI_SGDS = 7, EPI_ADAMS = 8, EPI_SGDS_T = 9, EPI_STORE_T = 10, EPI_STORE_DT = 11 };
-__host__ __device__ constexpr bool epi_tout(int e) { return e == EPI_SGDS_T || e == EPI_STORE_T; }
+                 EPI_SGDS = 7, EPI_ADAMS = 8, EPI_SGDS_T = 9, EPI_STORE_T = 10, EPI_STORE_DT = 11, EPI_ADAMS_T = 12 };
+__host__ __device__ constexpr bool epi_tout(int e) { return e == EPI_SGDS_T || e == EPI_STORE_T || e == EPI_ADAMS_T; }
 enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_SILU = 2, ACT_GELU = 3 };
 
 __device__ __forceinline__ float bf2f(uint16_t v) {

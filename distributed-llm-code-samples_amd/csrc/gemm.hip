@@ -61,13 +61,14 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
   const bool aligned_ptr = ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && ((uintptr_t)C % 16 == 0) &&
                            ((uintptr_t)aux % 16 == 0) && ((uintptr_t)aux_out % 16 == 0) &&
                            ((uintptr_t)opt_m % 16 == 0) && ((uintptr_t)opt_v % 16 == 0);
-  const bool opt_epi = (epi == EPI_SGD || epi == EPI_ADAM || epi == EPI_SGDS || epi == EPI_ADAMS || epi == EPI_SGDS_T);
-  const bool split_epi = (epi == EPI_SGDS || epi == EPI_ADAMS || epi == EPI_SGDS_T);
+  const bool opt_epi = (epi == EPI_SGD || epi == EPI_ADAM || epi == EPI_SGDS || epi == EPI_ADAMS || epi == EPI_SGDS_T ||
+                        epi == EPI_ADAMS_T);
+  const bool split_epi = (epi == EPI_SGDS || epi == EPI_ADAMS || epi == EPI_SGDS_T || epi == EPI_ADAMS_T);
   if (opt_epi && layout == L_NT) return -1;
   if ((epi == EPI_SGD || epi == EPI_ADAM) && out_dtype != DT_F32) return -1;
   // split master: C = the 16-bit residual plane, aux_out = the bf16 working copy (paired 16-B rows: ld % 8 == 0)
   if (split_epi && (out_dtype != DT_BF16 || in_dtype != DT_BF16 || aux_out == nullptr)) return -1;
-  if (epi == EPI_ADAM || epi == EPI_ADAMS) {
+  if (epi == EPI_ADAM || epi == EPI_ADAMS || epi == EPI_ADAMS_T) {
     if (step < 1 || !opt_m || !opt_v) return -1;
     a.bc1 = 1.f - powf(b1, (float)step);
     a.bc2 = 1.f - powf(b2, (float)step);
@@ -92,14 +93,14 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
   hipError_t e;
   // The NN weight-gradient layout (transposed outputs, transposed copies, NN fused SGD on 256-row tiles):
   // 8-phase 256x256 persistent kernels only (gemm_kernels.h dispatch_x)
-  const bool xepi = epi == EPI_SGDS_T || epi == EPI_STORE_T || epi == EPI_STORE_DT;
-  if (xepi || (epi == EPI_SGDS && layout == L_NN && path == 0)) {
+  const bool xepi = epi == EPI_SGDS_T || epi == EPI_STORE_T || epi == EPI_STORE_DT || epi == EPI_ADAMS_T;
+  if (xepi || ((epi == EPI_SGDS || epi == EPI_ADAMS) && layout == L_NN && path == 0)) {
     if (path != 0 || K % (2 * BT_K) != 0 || ksplit > 1 || mask != nullptr || beta != 0.f || ldc % 8 != 0 ||
         (a.variant != 0 && a.variant != 3))
       return -1;
     if (epi == EPI_STORE_DT && (aux_out == nullptr || out_dtype != DT_BF16 || ldaux % 8 != 0 || layout == L_TN))
       return -1;
-    if ((epi == EPI_SGDS || epi == EPI_SGDS_T) && layout != L_NN) return -1;
+    if (opt_epi && layout != L_NN) return -1;
     e = layout == L_NN ? dispatch_nn_x(epi, a, out_dtype, s)
         : layout == L_NT ? dispatch_nt_x(epi, a, out_dtype, s) : dispatch_tn_x(epi, a, out_dtype, s);
     return (int)e;
@@ -180,7 +181,7 @@ int dllm_gemm_pair(int layout, int out_dtype, int epi, const void* const* A, con
     g.M = M[i]; g.N = N[i]; g.K = K; g.alpha = alpha; g.beta = 0.f; g.act = ACT_NONE; g.group_m = 4;
     g.lr = lr; g.b1 = b1; g.b2 = b2; g.eps = eps; g.wd = wd; g.opt_m = opt_m[i]; g.opt_v = opt_v[i];
     g.bc1 = 1.f; g.bc2 = 1.f;
-    if (epi == EPI_ADAM || epi == EPI_ADAMS) {
+    if (epi == EPI_ADAM || epi == EPI_ADAMS || epi == EPI_ADAMS_T) {
       g.bc1 = 1.f - powf(b1, (float)step);
       g.bc2 = 1.f - powf(b2, (float)step);
     }

@@ -341,7 +341,7 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
   constexpr int COST = EPI == EPI_DACT ? WR : EPI == EPI_DGLU ? 8 * (BF ? 2 : 4)
                      : EPI == EPI_STORE || EPI == EPI_STORE_T || EPI == EPI_STORE_DT ? 4 * WR
                      : EPI == EPI_SGD || EPI == EPI_SGDS || EPI == EPI_SGDS_T ? 8
-                     : EPI == EPI_ADAM || EPI == EPI_ADAMS ? 24 : 0;
+                     : EPI == EPI_ADAM || EPI == EPI_ADAMS || EPI == EPI_ADAMS_T ? 24 : 0;
   constexpr int RB = epi_batch(COST);
   const int pc = pair_col(lane);
 #define DLLM_M(rg) (m0 + ((rg) >> 3) * 128 + wr * ((BM != 256 && ((rg) >> 3)) ? 48 : 64) + ((rg) & 3) * 16 + (lane & 15))
@@ -674,9 +674,9 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
             pair_swap(uint2{lw[0], lw[1]}, uint2{lw[2], lw[3]});
       }
     }
-  } else if constexpr (EPI == EPI_ADAMS) {
+  } else if constexpr (EPI == EPI_ADAMS || EPI == EPI_ADAMS_T) {
     // split master + fp32 moments: per row group one paired 16-B access per plane and two 16-B moment accesses per
-    // fragment (24 B per parameter instead of 26 B)
+    // fragment (24 B per parameter instead of 26 B).  EPI_ADAMS_T: the transposed map (row_of / colb_of / acc_of)
 #pragma unroll
     for (int b0 = 0; b0 < 16; b0 += RB) {
       uint4 H[RB], Lw[RB];
@@ -684,11 +684,11 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
 #pragma unroll
       for (int r = 0; r < RB; ++r) {
         if (!DLLM_OK(b0 + r)) continue;
-        H[r] = *(const uint4*)((const uint16_t*)p.aux_out + (long)DLLM_M(b0 + r) * p.ldaux + DLLM_NB(b0 + r) + pc);
-        Lw[r] = *(const uint4*)((const uint16_t*)Cp + (long)DLLM_M(b0 + r) * p.ldc + DLLM_NB(b0 + r) + pc);
+        H[r] = *(const uint4*)((const uint16_t*)p.aux_out + (long)row_of(b0 + r) * p.ldaux + colb_of(b0 + r) + pc);
+        Lw[r] = *(const uint4*)((const uint16_t*)Cp + (long)row_of(b0 + r) * p.ldc + colb_of(b0 + r) + pc);
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) {
-          const long ci = (long)DLLM_M(b0 + r) * p.ldc + DLLM_N(b0 + r, nt);
+          const long ci = (long)row_of(b0 + r) * p.ldc + colb_of(b0 + r) + nt * 16 + 4 * (lane >> 4);
           Mm[r][nt] = RF::load(p.opt_m, ci);
           Vv[r][nt] = RF::load(p.opt_v, ci);
         }
@@ -702,7 +702,7 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int nt = j >> 1, e = 2 * (j & 1);
-          const f32x4_t gg = DLLM_ACC(b0 + r, nt);
+          const f32x4_t gg = acc_of(b0 + r, nt);
           float f0, f1;
           split_join2(hw[j], lw[j], f0, f1);
           float m0 = Mm[r][nt][e], v0 = Vv[r][nt][e], m1 = Mm[r][nt][e + 1], v1 = Vv[r][nt][e + 1];
@@ -714,13 +714,13 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
           Vv[r][nt][e + 1] = v1;
           split_part2(f0, f1, hw[j], lw[j]);
         }
-        *(uint4*)((uint16_t*)p.aux_out + (long)DLLM_M(b0 + r) * p.ldaux + DLLM_NB(b0 + r) + pc) =
+        *(uint4*)((uint16_t*)p.aux_out + (long)row_of(b0 + r) * p.ldaux + colb_of(b0 + r) + pc) =
             pair_swap(uint2{hw[0], hw[1]}, uint2{hw[2], hw[3]});
-        *(uint4*)((uint16_t*)Cp + (long)DLLM_M(b0 + r) * p.ldc + DLLM_NB(b0 + r) + pc) =
+        *(uint4*)((uint16_t*)Cp + (long)row_of(b0 + r) * p.ldc + colb_of(b0 + r) + pc) =
             pair_swap(uint2{lw[0], lw[1]}, uint2{lw[2], lw[3]});
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) {
-          const long ci = (long)DLLM_M(b0 + r) * p.ldc + DLLM_N(b0 + r, nt);
+          const long ci = (long)row_of(b0 + r) * p.ldc + colb_of(b0 + r) + nt * 16 + 4 * (lane >> 4);
           Vec4<float>::store(p.opt_m, ci, Mm[r][nt]);
           Vec4<float>::store(p.opt_v, ci, Vv[r][nt]);
         }
@@ -2128,13 +2128,14 @@ static hipError_t launch_splitk(const GemmArgs& a, int out_dt, float* ws, hipStr
 template <int L, int E, typename OutT, int ACT>
 constexpr bool persistent_kernel() {
   constexpr bool bf = std::is_same<OutT, uint16_t>::value;
+  if constexpr (E == EPI_ADAMS_T) return false;   // fused AdamW: one tile per block (see above)
   if constexpr (E == EPI_STORE_DT || E == EPI_STORE_T || E == EPI_SGDS_T) return true;
   if constexpr (L == L_NN && E == EPI_SGDS) return true;   // the NN weight-gradient layout (dispatch_x)
   // gated (SwiGLU) stacks: the GLU forward / DGLU dgrad with a compile-time activation (round 3)
   // NT dgrad with the ReLU mask: W2 stored as W2ᵀ (the nn_w2t weight-gradient mode, parallel/engine.py)
   if constexpr (L == L_NT)
     return bf && ((E == EPI_ACT && ACT == ACT_RELU) || E == EPI_STORE || (E == EPI_GLU && ACT >= 0) ||
-                  (E == EPI_DACT && ACT == ACT_RELU));
+                  (E == EPI_DACT && ACT == ACT_RELU) || (E == EPI_DGLU && ACT >= 0));
   if constexpr (L == L_NN) return bf && ((E == EPI_DACT && ACT == ACT_RELU) || E == EPI_STORE || (E == EPI_DGLU && ACT >= 0));
   return E == EPI_STORE || E == EPI_SGD || E == EPI_SGDS;
 }
@@ -2157,9 +2158,13 @@ static hipError_t dispatch_x(int epi, const GemmArgs& a, int out_dt, hipStream_t
       break;
     case EPI_SGDS_T:
     case EPI_SGDS:
+    case EPI_ADAMS_T:
+    case EPI_ADAMS:
       if constexpr (L == L_NN) {
         if (epi == EPI_SGDS) launch_8ph_act<L, EPI_SGDS, float, -1, 8>(a, nb, s);
-        else launch_8ph_act<L, EPI_SGDS_T, float, -1, 8>(a, nb, s);
+        else if (epi == EPI_SGDS_T) launch_8ph_act<L, EPI_SGDS_T, float, -1, 8>(a, nb, s);
+        else if (epi == EPI_ADAMS) launch_8ph_act<L, EPI_ADAMS, float, -1, 8>(a, nb, s);
+        else launch_8ph_act<L, EPI_ADAMS_T, float, -1, 8>(a, nb, s);
         break;
       } else {
         return hipErrorInvalidValue;
@@ -2185,7 +2190,8 @@ static void launch_8ph_act(const GemmArgs& a0, int nb0, hipStream_t s) {
 template <int L, int E, typename OutT, int NPH>
 static void launch_8ph_stagger(const GemmArgs& a, int nb, hipStream_t s) {
   constexpr bool fwd = L == L_NT && (E == EPI_ACT || E == EPI_GLU);
-  constexpr bool bwd = (L == L_NN && (E == EPI_DACT || E == EPI_DGLU)) || (L == L_NT && E == EPI_DACT && NPH == 8);
+  constexpr bool bwd = (L == L_NN && (E == EPI_DACT || E == EPI_DGLU)) ||
+                       (L == L_NT && (E == EPI_DACT || E == EPI_DGLU) && NPH == 8);
   if constexpr ((fwd || bwd) && std::is_same<OutT, uint16_t>::value) {
     switch (a.act) {
       case ACT_RELU: launch_8ph_act<L, E, OutT, ACT_RELU, NPH>(a, nb, s); return;

@@ -171,8 +171,7 @@ def layer_bwd(dy: torch.Tensor, x: torch.Tensor, w1: torch.Tensor, w2: torch.Ten
     """
     w2_layout = "nt" if nn is not None and nn.w2t else "nn"           # w2t: w2 is the stored W2ᵀ [F, D]
     if gated:
-        assert w2_layout == "nn", "gated layers keep W2 row-major"
-        gemm(dy, w2, "nn", out=da_buf, epi="dglu", act=act, aux=h)    # [dg|du] interleaved [T, 2F]
+        gemm(dy, w2, w2_layout, out=da_buf, epi="dglu", act=act, aux=h)   # [dg|du] interleaved [T, 2F]
     else:
         gemm(dy, w2, w2_layout, out=da_buf, epi="dact", act=act, aux=h if h is not None else a, mask=mask)
     kw1 = gw1 if isinstance(gw1, dict) else {"out": gw1}

@@ -24,7 +24,8 @@ followed by an epilogue:
 
 Transposed outputs (the NN weight-gradient layout, ``ffn.layer_bwd(..., wgrad_nn=...)``; 256x256 8-phase tiles):
 
-* ``out_t=True`` (``"store"`` in any layout, ``"sgd_split"`` in ``"nn"``): ``out`` (and ``aux_out``) hold ``Cᵀ``
+* ``out_t=True`` (``"store"`` in any layout, ``"sgd_split"`` / ``"adam_split"`` in ``"nn"``): ``out`` (and ``aux_out``,
+  the moments) hold ``Cᵀ``
   [N, M] -- e.g.
   ``dW1ᵀ = xᵀ·da`` written into (or updating) ``W1`` [F, D] while ``xᵀ`` is the K-contiguous A operand
 * ``aux_t=`` (``"store"``, beta 0, bf16, layouts ``"nt"`` / ``"nn"``): also writes ``Cᵀ`` [N, M] into ``aux_t`` --
@@ -301,7 +302,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
     # fused optimizers: the weight-gradient layouts -- TN, NN on 224-row tiles (transposed-activation TP layout), or
     # the NN weight-gradient layout's 256x256 tiles (split masters)
     opt_layout_ok = layout == "tn" or (layout == "nn" and a.device.type == "cuda" and (
-        use_m224(M, N) or (epi == "sgd_split" and nn_wgrad_supported(M, N, K))))
+        use_m224(M, N) or (epi in ("sgd_split", "adam_split") and nn_wgrad_supported(M, N, K))))
     if epi in ("sgd", "adam"):
         if not (opt_layout_ok or (layout == "nn" and a.device.type != "cuda")) or out.dtype != torch.float32:
             raise ValueError("fused-optimizer epilogues need the TN (weight-gradient) layout and an fp32 master")
@@ -380,7 +381,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
     return out
 
 
-EPI_T = {"store": 10, "sgd_split": 9}     # csrc/common.h EPI_STORE_T / EPI_SGDS_T
+EPI_T = {"store": 10, "sgd_split": 9, "adam_split": 12}     # csrc/common.h EPI_STORE_T / EPI_SGDS_T / EPI_ADAMS_T
 EPI_STORE_DT = 11
 
 
@@ -394,7 +395,7 @@ def _check_transposed(a, layout, epi, M, N, K, out_t, aux_t, beta) -> None:
     if out_t and aux_t is not None:
         raise ValueError("out_t and aux_t are exclusive")
     if out_t and (epi not in EPI_T or (epi != "store" and layout != "nn")):
-        raise ValueError(f"out_t: 'store' (any layout) or 'sgd_split' (NN layout) only (got {epi}, {layout})")
+        raise ValueError(f"out_t: 'store' (any layout) or the split-master optimizers (NN layout) only (got {epi}, {layout})")
     if aux_t is not None and (epi != "store" or layout not in ("nt", "nn")):
         raise ValueError(f"aux_t: the store epilogue in the NT / NN layouts only (got {epi}, {layout})")
     if beta != 0.0:

@@ -238,7 +238,7 @@ class FFNTrainer:
         mode = "nn_w2t" if cfg.wgrad_layout == "auto" else cfg.wgrad_layout
         self.wgrad_nn = self._wgrad_nn_supported() and mode in ("nn", "nn_w1", "nn_w2t")   # dW1 as NN (out_t)
         self.wgrad_nn_w2 = self.wgrad_nn and mode in ("nn", "nn_w2t")                        # dW2 as NN too
-        self.w2t_nn = self.wgrad_nn and mode == "nn_w2t" and not self.gated
+        self.w2t_nn = self.wgrad_nn and mode == "nn_w2t"
         # W2 stored as W2ᵀ [F_loc, D]: the transposed-activation TP layout, or the nn_w2t weight-gradient mode
         self.w2t = self.tmode or self.w2t_nn
 
@@ -444,7 +444,7 @@ class FFNTrainer:
     def _wgrad_nn_supported(self) -> bool:
         """Whether the weight gradients run in the NN layout (``cfg.wgrad_layout``; models/ffn.NNWgrad): GPU, bf16, the
         plain row-major layer (no TP / SP / FSDP / transposed-activation mode / recompute / grouped pair / TP chunks),
-        256x256 8-phase shapes, and a fused optimizer only as SGD on split masters (stored gradients: any)."""
+        256x256 8-phase shapes, and a fused optimizer only on split masters (SGD / AdamW; stored gradients: any)."""
         cfg = self.cfg
         if cfg.wgrad_layout not in ("auto", "tn", "nn", "nn_w1", "nn_w2t"):
             raise ValueError(f"unknown wgrad_layout {cfg.wgrad_layout!r}")
@@ -460,8 +460,8 @@ class FFNTrainer:
             why.append("row-major data-parallel / single-device layers only")
         if cfg.recompute != "none":
             why.append("kept activations only")
-        if self.fused_opt and not (self.split and cfg.optimizer == "sgd"):
-            why.append("fused optimizer: SGD on split masters only")
+        if self.fused_opt and not self.split:
+            why.append("fused optimizer: split masters only")
         if not (nn_wgrad_supported(D, self.F_loc, T) and nn_wgrad_supported(D, self.R1, T) and T % 64 == 0):
             why.append(f"shapes (D={D}, F={self.F_loc}, T={T}) off the 256x256 8-phase tiles")
         elif (choose_ksplit(D, self.F_loc, T) > 1 or choose_ksplit(self.R1, D, T) > 1
@@ -584,7 +584,7 @@ class FFNTrainer:
         if self.da_free[l % 2] is not None:
             main.wait_event(self.da_free[l % 2])
         if self.gated:   # [dg|du] interleaved [T, 2F] (as layer_bwd)
-            gemm(g, w2, "nn", out=da, epi="dglu", act=act, aux=h)
+            gemm(g, w2, "nt" if self.w2t_nn else "nn", out=da, epi="dglu", act=act, aux=h)
         else:
             gemm(g, w2, "nt" if self.w2t_nn else "nn", out=da, epi="dact", act=act, aux=h if h is not None else a,
                  mask=self._mask(l))

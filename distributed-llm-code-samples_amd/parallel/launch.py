@@ -168,6 +168,9 @@ def run_rank(rank: int, world: int, cfg_dict: dict, method: int, backend: str, p
                             "grads": eng.grads.numel(),
                             "adam": eng.adam_m.numel() if getattr(eng, "adam_m", None) is not None else 0},
             "ckpt_bytes_read_max": read_max,
+            # GEMM layouts the engine chose (parallel/engine.py): NN weight gradients, W2 stored transposed
+            "layout": {"wgrad_nn": bool(eng.wgrad_nn), "wgrad_nn_w2": bool(eng.wgrad_nn_w2), "w2t": bool(eng.w2t),
+                       "tp_transposed": bool(eng.tmode)},
         }
         if opts.get("count_collectives") and steps > 0:
             rec["collectives_per_step"] = {r: c / steps for r, c in counter.by_role(mesh.groups).items()}

@@ -75,8 +75,8 @@ class TrainConfig:
     # weight-gradient GEMM layout: "tn" (dW = dyᵀ·a, daᵀ·x: both operands through transposed LDS reads), "nn"
     # (transposed copies xᵀ / dyᵀ [D, T] from the producing epilogues; models/ffn.NNWgrad), "nn_w1" (dW1 only: xᵀ
     # copies; dW2 stays TN) or "nn_w2t" (nn with W2 stored as W2ᵀ [F, D]: both weight gradients written through the
-    # transposed map); "auto" = nn_w2t where the engine supports it (GPU, bf16, 256x256 8-phase shapes, no TP / SP /
-    # FSDP / recompute, SGD on split masters or stored gradients; gated stacks keep W2 row-major)
+    # transposed map); "auto" = nn_w2t where the engine supports it (GPU, bf16, 256x256 8-phase shapes without split-K,
+    # no TP / SP / FSDP / recompute, fused SGD / AdamW on split masters or stored gradients)
     wgrad_layout: str = "auto"
     wgrad_stream: bool = False       # single device, fused optimizer: weight-gradient GEMMs on a second
                                      # stream, concurrent with the dgrad chain (CUs shared; epilogues overlap)

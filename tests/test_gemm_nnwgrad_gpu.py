@@ -69,6 +69,27 @@ def test_nn_fused_sgd_matches_tn(T, D, F):
 
 
 @pytest.mark.parametrize("T,D,F", SHAPES)
+def test_nn_fused_adamw_matches_tn(T, D, F):
+    """The split-master AdamW epilogue through the transposed map (EPI_ADAMS_T, dW1 into W1 [F, D]) and on NN 256x256
+    tiles (dW2): masters and moments bitwise the TN kernel's."""
+    g = torch.Generator().manual_seed(6)
+    dy, a, da, x = _rnd(g, T, D), _rnd(g, T, F), _rnd(g, T, F), _rnd(g, T, D)
+    kw = dict(epi="adam_split", lr=1e-3, betas=(0.9, 0.95), eps=1e-8, wd=0.1, step=3)
+    for shape, tn, nn in (((D, F), lambda **k: gemm(dy, a, "tn", **k),
+                           lambda **k: gemm(dy.t().contiguous(), a, "nn", **k)),
+                          ((F, D), lambda **k: gemm(da, x, "tn", **k),
+                           lambda **k: gemm(x.t().contiguous(), da, "nn", out_t=True, **k))):
+        m = (torch.randn(*shape, generator=g) * 0.02).cuda()
+        mom = (torch.randn(*shape, generator=g) * 1e-3).cuda(), (torch.rand(*shape, generator=g) * 1e-5).cuda()
+        h0, l0 = split_master(m)
+        st = [(h0, l0, mom[0].clone(), mom[1].clone()), (h0.clone(), l0.clone(), mom[0].clone(), mom[1].clone())]
+        for (h, lo, mm, vv), fn in zip(st, (tn, nn)):
+            fn(out=lo, aux_out=h, opt_m=mm, opt_v=vv, **kw)
+        for u, v in zip(st[0], st[1]):
+            assert torch.equal(u, v), shape
+
+
+@pytest.mark.parametrize("T,D,F", SHAPES)
 @pytest.mark.parametrize("layout", ["nt", "nn"])
 def test_store_with_transposed_copy(T, D, F, layout):
     """y = a·W2ᵀ (NT) and dx = da·W1 (NN) with ``aux_t``: the output is bitwise the plain store's and the copy is
@@ -108,7 +129,8 @@ def test_transposed_outputs_reject_bad_shapes():
         gemm(a, a, "tn", out_t=True, epi="sgd_split")    # transposed fused optimizer: NN only
 
 
-@pytest.mark.parametrize("variant", ["fused_serial", "fused_wgrad_stream", "grads_fp32", "grads_bf16"])
+@pytest.mark.parametrize("variant", ["fused_serial", "fused_wgrad_stream", "grads_fp32", "grads_bf16",
+                                     "gated_adamw"])
 def test_engine_nn_wgrad_layout_bitwise_tn(variant, monkeypatch):
     """Three layers, three steps: the engine's NN weight-gradient layout (transposed copies from the fwd-2 / dx
     epilogues and the step-start transposes) leaves masters bitwise equal to the TN layout's -- fused split-master SGD
@@ -122,18 +144,20 @@ def test_engine_nn_wgrad_layout_bitwise_tn(variant, monkeypatch):
 
     monkeypatch.setenv("DLLM_NN_CONCURRENT", "1")   # keep the (A/B-only) concurrent NN path covered
     dev = torch.device("cuda", 0)
-    m = ModelConfig(model_size=2048, ffn_dim=8192, layers=3, act="relu")   # tile grids too big for the pair
+    gated = variant == "gated_adamw"    # SwiGLU + fused AdamW on split masters (config 5's kind)
+    m = ModelConfig(model_size=2048, ffn_dim=8192, layers=3, act="silu" if gated else "relu", gated=gated)
     out = {}
     for layout in ("tn", "nn", "nn_w1", "nn_w2t"):
         cfg = TrainConfig(model=m, batch_size=1, seq_len=1024, dtype="bf16",
-                          grad_dtype="bf16" if variant == "grads_bf16" else "fp32", optimizer="sgd", lr=1e-3,
+                          grad_dtype="bf16" if variant == "grads_bf16" else "fp32",
+                          optimizer="adam" if gated else "sgd", lr=1e-3,
                           wgrad_layout=layout, wgrad_stream=variant == "fused_wgrad_stream",
-                          fused_optimizer=variant.startswith("fused"))
+                          fused_optimizer=variant.startswith("fused") or gated)
         eng = FFNTrainer(cfg, Mesh(), dev)
         assert eng.wgrad_nn == (layout != "tn") and eng.wgrad_nn_w2 == (layout in ("nn", "nn_w2t"))
         assert eng.w2t == (layout == "nn_w2t")
         assert (eng.wg_stream is not None) == (variant == "fused_wgrad_stream")
-        eng.load_full_params(init_ffn_params_device(m.D, m.F, m.layers, 7, dev))
+        eng.load_full_params(init_ffn_params_device(m.D, m.F, m.layers, 7, dev, gated=gated))
         data = DeviceMockData(cfg.tokens, m.D, torch.bfloat16, dev)
         ys = []
         for i in range(3):

@@ -22,10 +22,11 @@ def _cfg(D, F, L, T, steps=4, **kw):  # steps divisible by dp (train_ffns.py:175
                        lr=kw.pop("lr", 1e-2), data="cpu_compat", **kw)
 
 
-def _run(cfg, method, n, port, **opts):
+def _run(cfg, method, n, port, record=False, **opts):
     o = {"seed": SEED, "init": "cpu_compat", "return_full": True, "tp": opts.pop("tp", n), "device": "cuda"}
     o.update(opts)
-    return spawn(n, cfg, method, "gloo", port, o, timeout_s=240)["params"]
+    rec = spawn(n, cfg, method, "gloo", port, o, timeout_s=240)
+    return rec if record else rec["params"]
 
 
 def _oracle(cfg, n):
@@ -97,3 +98,29 @@ def test_tp_transposed_layout_two_ranks_and_checkpoint_crossing(free_port, tmp_p
         _run(src, 4, 2, free_port + 2 + 2 * i, ckpt_dir=d, ckpt_format="sharded", stop_after=2)
         resumed = _run(dst, 4, 2, free_port + 3 + 2 * i, resume=d)
         _close(resumed, on, rtol=2e-2, atol=1e-4)
+
+
+def test_nn_weight_gradient_layout_two_ranks_and_checkpoint_crossing(free_port, tmp_path):
+    """The NN weight-gradient layout (nn_w2t: W2 stored transposed, transposed xᵀ / dyᵀ copies, stored gradients
+    through the transposed map) on 2 real DDP / ZeRO-2 ranks: bitwise the TN layout's masters; a sharded ZeRO
+    checkpoint written in one layout resumes in the other (both directions).  Shapes large enough that no GEMM of the
+    layer takes split-K (the engine's condition for the NN layout)."""
+    base = dict(dtype="bf16", grad_dtype="bf16", lr=1e-3)
+    D, F, L, T = 2048, 8192, 2, 8192
+    nn = _cfg(D, F, L, T, wgrad_layout="nn_w2t", **base)
+    tn = _cfg(D, F, L, T, wgrad_layout="tn", **base)
+    port = free_port
+    ref = {}
+    for method in (2, 6):                          # DDP, ZeRO-2
+        ra = _run(nn, method, 2, port, record=True)
+        rb = _run(tn, method, 2, port + 1, record=True)
+        port += 2
+        assert ra["layout"]["wgrad_nn_w2"] and ra["layout"]["w2t"] and not rb["layout"]["wgrad_nn"]
+        assert _equal(ra["params"], rb["params"]), method
+        ref[method] = rb["params"]
+    for i, (src, dst) in enumerate(((nn, tn), (tn, nn))):
+        d = str(tmp_path / f"ck{i}")
+        _run(src, 6, 2, port, ckpt_dir=d, ckpt_format="sharded", stop_after=2)
+        resumed = _run(dst, 6, 2, port + 1, resume=d)
+        port += 2
+        assert _equal(resumed, ref[6]), i
