@@ -100,7 +100,7 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
       return -1;
     if (epi == EPI_STORE_DT && (aux_out == nullptr || out_dtype != DT_BF16 || ldaux % 8 != 0 || layout == L_TN))
       return -1;
-    if (opt_epi && layout != L_NN) return -1;
+    if (opt_epi && !(layout == L_NN || (layout == L_TN && epi_tout(epi)))) return -1;
     e = layout == L_NN ? dispatch_nn_x(epi, a, out_dtype, s)
         : layout == L_NT ? dispatch_nt_x(epi, a, out_dtype, s) : dispatch_tn_x(epi, a, out_dtype, s);
     return (int)e;

@@ -2166,6 +2166,11 @@ static hipError_t dispatch_x(int epi, const GemmArgs& a, int out_dt, hipStream_t
         else if (epi == EPI_ADAMS) launch_8ph_act<L, EPI_ADAMS, float, -1, 8>(a, nb, s);
         else launch_8ph_act<L, EPI_ADAMS_T, float, -1, 8>(a, nb, s);
         break;
+      } else if constexpr (L == L_TN) {   // W2 stored transposed with TN weight gradients (--w2_storage transposed)
+        if (epi == EPI_SGDS_T) launch_8ph_act<L, EPI_SGDS_T, float, -1, 8>(a, nb, s);
+        else if (epi == EPI_ADAMS_T) launch_8ph_act<L, EPI_ADAMS_T, float, -1, 8>(a, nb, s);
+        else return hipErrorInvalidValue;
+        break;
       } else {
         return hipErrorInvalidValue;
       }

@@ -126,16 +126,15 @@ class NNWgrad(NamedTuple):
     x_t: torch.Tensor
     dy_t: torch.Tensor | None
     dx_t: torch.Tensor | None
-    w2t: bool = False    # W2 stored as W2ᵀ [F, D] (nn_w2t): dW2ᵀ written through the transposed map, dgrad NT
 
 
-def wgrad_w2(dy: torch.Tensor, a: torch.Tensor, kw2: dict, nn: NNWgrad | None) -> None:
+def wgrad_w2(dy: torch.Tensor, a: torch.Tensor, kw2: dict, nn: NNWgrad | None, w2t: bool = False) -> None:
+    """dW2 [D, F]; ``w2t``: W2 is stored as W2ᵀ [F, D] and the gradient / fused update goes through the transposed
+    output map (``gemm(out_t=True)``)."""
     if nn is None or nn.dy_t is None:
-        gemm(dy, a, "tn", **kw2)                                      # dW2 = dyᵀ·a        [D, F]
-    elif nn.w2t:
-        gemm(nn.dy_t, a, "nn", out_t=True, **kw2)                     # dW2 = (dyᵀ)·a      -> W2ᵀ [F, D]
+        gemm(dy, a, "tn", out_t=w2t, **kw2)                           # dW2 = dyᵀ·a        [D, F] (or -> W2ᵀ)
     else:
-        gemm(nn.dy_t, a, "nn", **kw2)                                 # dW2 = (dyᵀ)·a      [D, F]
+        gemm(nn.dy_t, a, "nn", out_t=w2t, **kw2)                      # dW2 = (dyᵀ)·a      [D, F] (or -> W2ᵀ)
 
 
 def wgrad_w1(da: torch.Tensor, x: torch.Tensor, kw1: dict, nn: NNWgrad | None) -> None:
@@ -149,7 +148,7 @@ def layer_bwd(dy: torch.Tensor, x: torch.Tensor, w1: torch.Tensor, w2: torch.Ten
               a: torch.Tensor, h: torch.Tensor | None, gw1, gw2, da_buf: torch.Tensor,
               dx_out: torch.Tensor | None, hooks=None, mask: torch.Tensor | None = None,
               dx_first: bool = False, pair_wgrads: bool = False,
-              nn: NNWgrad | None = None) -> torch.Tensor | None:
+              nn: NNWgrad | None = None, w2t: bool = False) -> torch.Tensor | None:
     """Backward of one layer; returns dx.
 
     ``gw1``/``gw2`` are either gradient tensors (overwritten) or dicts of ``gemm`` keyword arguments for the
@@ -168,8 +167,9 @@ def layer_bwd(dy: torch.Tensor, x: torch.Tensor, w1: torch.Tensor, w2: torch.Ten
     and their reduction passes; dx still runs before W1's fused update, and a TP all-reduce of dx overlaps the pair.
 
     ``nn`` (``NNWgrad``): the weight gradients in the NN layout; dx's epilogue also writes dxᵀ into ``nn.dx_t``.
+    ``w2t``: ``w2`` is the stored W2ᵀ [F, D]: the dgrad runs NT and dW2 goes through the transposed output map.
     """
-    w2_layout = "nt" if nn is not None and nn.w2t else "nn"           # w2t: w2 is the stored W2ᵀ [F, D]
+    w2_layout = "nt" if w2t else "nn"                                  # w2t: w2 is the stored W2ᵀ [F, D]
     if gated:
         gemm(dy, w2, w2_layout, out=da_buf, epi="dglu", act=act, aux=h)   # [dg|du] interleaved [T, 2F]
     else:
@@ -177,6 +177,7 @@ def layer_bwd(dy: torch.Tensor, x: torch.Tensor, w1: torch.Tensor, w2: torch.Ten
     kw1 = gw1 if isinstance(gw1, dict) else {"out": gw1}
     kw2 = gw2 if isinstance(gw2, dict) else {"out": gw2}
     if pair_wgrads:
+        assert not w2t, "grouped weight-gradient pairs keep W2 row-major"
         dx = None
         if dx_out is not None:
             dx = gemm(da_buf, w1, "nn", out=dx_out)                   # dx = da·W1 (before W1's update)
@@ -198,7 +199,7 @@ def layer_bwd(dy: torch.Tensor, x: torch.Tensor, w1: torch.Tensor, w2: torch.Ten
         wgrad_w1(da_buf, x, kw1, nn)                                  # dW1 = daᵀ·x        [F, D]
         if hooks is not None:
             hooks.after_w1()
-        wgrad_w2(dy, a, kw2, nn)                                      # dW2 = dyᵀ·a        [D, F]
+        wgrad_w2(dy, a, kw2, nn, w2t)                                 # dW2 = dyᵀ·a        [D, F]
         if hooks is not None:
             hooks.after_w2()
         return None
@@ -206,7 +207,7 @@ def layer_bwd(dy: torch.Tensor, x: torch.Tensor, w1: torch.Tensor, w2: torch.Ten
         dx = gemm(da_buf, w1, "nn", out=dx_out, aux_t=dx_t)           # dx = da·W1         [T, D]
         if hooks is not None:
             hooks.after_dx(dx)
-    wgrad_w2(dy, a, kw2, nn)                                          # dW2 = dyᵀ·a        [D, F]
+    wgrad_w2(dy, a, kw2, nn, w2t)                                     # dW2 = dyᵀ·a        [D, F]
     if hooks is not None:
         hooks.after_w2()
     if not dx_first:

@@ -24,7 +24,8 @@ followed by an epilogue:
 
 Transposed outputs (the NN weight-gradient layout, ``ffn.layer_bwd(..., wgrad_nn=...)``; 256x256 8-phase tiles):
 
-* ``out_t=True`` (``"store"`` in any layout, ``"sgd_split"`` / ``"adam_split"`` in ``"nn"``): ``out`` (and ``aux_out``,
+* ``out_t=True`` (``"store"`` in any layout, ``"sgd_split"`` / ``"adam_split"`` in ``"nn"`` / ``"tn"``; any epilogue on
+  the CPU reference): ``out`` (and ``aux_out``,
   the moments) hold ``Cᵀ``
   [N, M] -- e.g.
   ``dW1ᵀ = xᵀ·da`` written into (or updating) ``W1`` [F, D] while ``xᵀ`` is the K-contiguous A operand
@@ -394,8 +395,8 @@ def nn_wgrad_supported(M: int, N: int, K: int) -> bool:
 def _check_transposed(a, layout, epi, M, N, K, out_t, aux_t, beta) -> None:
     if out_t and aux_t is not None:
         raise ValueError("out_t and aux_t are exclusive")
-    if out_t and (epi not in EPI_T or (epi != "store" and layout != "nn")):
-        raise ValueError(f"out_t: 'store' (any layout) or the split-master optimizers (NN layout) only (got {epi}, {layout})")
+    if out_t and a.device.type == "cuda" and (epi not in EPI_T or (epi != "store" and layout == "nt")):
+        raise ValueError(f"out_t: 'store' (any layout) or the split-master optimizers (NN / TN) only (got {epi}, {layout})")
     if aux_t is not None and (epi != "store" or layout not in ("nt", "nn")):
         raise ValueError(f"aux_t: the store epilogue in the NT / NN layouts only (got {epi}, {layout})")
     if beta != 0.0:

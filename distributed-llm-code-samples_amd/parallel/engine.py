@@ -238,9 +238,16 @@ class FFNTrainer:
         mode = "nn_w2t" if cfg.wgrad_layout == "auto" else cfg.wgrad_layout
         self.wgrad_nn = self._wgrad_nn_supported() and mode in ("nn", "nn_w1", "nn_w2t")   # dW1 as NN (out_t)
         self.wgrad_nn_w2 = self.wgrad_nn and mode in ("nn", "nn_w2t")                        # dW2 as NN too
-        self.w2t_nn = self.wgrad_nn and mode == "nn_w2t"
-        # W2 stored as W2ᵀ [F_loc, D]: the transposed-activation TP layout, or the nn_w2t weight-gradient mode
-        self.w2t = self.tmode or self.w2t_nn
+        # W2 stored as W2ᵀ [F_loc, D] in the row-major layer (self.w2s): the nn_w2t mode, or forced by cfg.w2_storage
+        # (any wgrad layout: the TN weight gradient then writes through the transposed map too; CPU tests of the
+        # storage, e.g. ZeRO-sharded checkpoints).  self.w2t: W2ᵀ storage in either layer form (tmode stores it too)
+        if cfg.w2_storage not in ("auto", "rowmajor", "transposed"):
+            raise ValueError(f"unknown w2_storage {cfg.w2_storage!r}")
+        self.w2s = not self.tmode and (cfg.w2_storage == "transposed" or
+                                       (cfg.w2_storage == "auto" and self.wgrad_nn and mode == "nn_w2t"))
+        if self.w2s and (self.tp_comm or self.sp or self.fsdp or self.pair_wgrads):
+            raise ValueError("w2_storage transposed: row-major data-parallel / single-device layers only")
+        self.w2t = self.tmode or self.w2s
 
         # ---- flat owned parameter layout (completion order) ------------------------------------
         full = {"w2": (self.F_loc, D) if self.w2t else (D, self.F_loc), "w1": (self.R1, D)}
@@ -584,19 +591,19 @@ class FFNTrainer:
         if self.da_free[l % 2] is not None:
             main.wait_event(self.da_free[l % 2])
         if self.gated:   # [dg|du] interleaved [T, 2F] (as layer_bwd)
-            gemm(g, w2, "nt" if self.w2t_nn else "nn", out=da, epi="dglu", act=act, aux=h)
+            gemm(g, w2, "nt" if self.w2s else "nn", out=da, epi="dglu", act=act, aux=h)
         else:
-            gemm(g, w2, "nt" if self.w2t_nn else "nn", out=da, epi="dact", act=act, aux=h if h is not None else a,
+            gemm(g, w2, "nt" if self.w2s else "nn", out=da, epi="dact", act=act, aux=h if h is not None else a,
                  mask=self._mask(l))
         e_da = torch.cuda.Event()
         e_da.record(main)
         side.wait_event(e_da)
         j = l % 3
         if self.wgrad_nn:
-            nn = NNWgrad(self.xT[l], gT, self.dxTb[j] if need_dx and self.wgrad_nn_w2 else None, self.w2t_nn)
+            nn = NNWgrad(self.xT[l], gT, self.dxTb[j] if need_dx and self.wgrad_nn_w2 else None)
         if need_dx:
             with torch.cuda.stream(side):
-                wgrad_w2(g, a, kw2, nn)                                   # dW2 = dyᵀ·a
+                wgrad_w2(g, a, kw2, nn, self.w2s)                         # dW2 = dyᵀ·a
                 e_dy = torch.cuda.Event()
                 e_dy.record(side)
             if self.dx_free[j] is not None:
@@ -609,7 +616,7 @@ class FFNTrainer:
         with torch.cuda.stream(side):
             wgrad_w1(da, self.xs[l], kw1, nn)                             # dW1 = daᵀ·x
             if not need_dx:
-                wgrad_w2(g, a, kw2, nn)                                   # layer 0: dW2 last
+                wgrad_w2(g, a, kw2, nn, self.w2s)                         # layer 0: dW2 last
             e_w = torch.cuda.Event()
             e_w.record(side)
         self.da_free[l % 2] = e_w
@@ -1170,7 +1177,7 @@ class FFNTrainer:
                 else:
                     layer_fwd(self.xs[l], w1, w2, act, gated, a, h, self.xs[l + 1], before_fwd2=before2,
                               mask=self._mask(l), y_t=self.xT[l + 1] if self.wgrad_nn and l + 1 < L else None,
-                              w2t=self.w2t_nn)
+                              w2t=self.w2s)
                 if self.tp_comm:
                     last = l == L - 1
                     if self.tp_car is not None:
@@ -1256,11 +1263,12 @@ class FFNTrainer:
             else:
                 if not keep:
                     recompute_fwd1(self.xs[l], w1, act, gated, a, h, mask=self._mask(l))
-                nn = (NNWgrad(self.xT[l], gT, self.dxTb[l % 2] if need_dx and self.wgrad_nn_w2 else None,
-                              self.w2t_nn) if self.wgrad_nn else None)
+                nn = (NNWgrad(self.xT[l], gT, self.dxTb[l % 2] if need_dx and self.wgrad_nn_w2 else None)
+                      if self.wgrad_nn else None)
                 dx = layer_bwd(g, self.xs[l], w1, w2, act, gated, a, h, gw1, gw2, self.da,
                                self.dxb[l % 2] if need_dx else None, hooks, mask=self._mask(l),
-                               dx_first=self.tp_comm and cfg.tp_overlap, pair_wgrads=self.pair_wgrads, nn=nn)
+                               dx_first=self.tp_comm and cfg.tp_overlap, pair_wgrads=self.pair_wgrads, nn=nn,
+                               w2t=self.w2s)
                 if dx is not None:
                     g = dx
                     gT = nn.dx_t if nn is not None else None

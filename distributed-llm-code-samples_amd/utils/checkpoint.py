@@ -76,6 +76,12 @@ def _local_geom(eng, name: str) -> tuple[int, int, int, int]:
     return eng.D, eng.F_loc, 0, r * eng.F_loc
 
 
+def _stored_t(eng, name: str) -> bool:
+    """Whether ``name`` is stored transposed (W2ᵀ [F_loc, D]: the transposed-activation TP layout or the row-major
+    layer's ``w2_storage``): its flat ranges are row-major in the STORED geometry, the checkpoint stays logical."""
+    return bool(getattr(eng, "w2t", False)) and name == "w2"
+
+
 def _flat_boxes(e0: int, e1: int, cols: int) -> list[tuple[int, int, int, int, int]]:
     """Split flat range [e0, e1) of a row-major ``[*, cols]`` tensor into boxes
     ``(r0, r1, c0, c1, flat_start)``: a partial first row, the full rows, a partial last row."""
@@ -100,6 +106,9 @@ def _owned_pieces(eng) -> list[dict]:
     for e in eng.entries:
         rows, cols, roff, coff = _local_geom(eng, e.name)
         base = {"layer": e.layer, "name": e.name, "rows": rows, "cols": cols, "row_off": roff, "col_off": coff}
+        if eng.zero and _stored_t(eng, e.name):
+            # flat ranges of the stored W2ᵀ: stored geometry [cols, rows] (``t``); boxes map back transposed
+            base.update(rows=cols, cols=rows, t=True)
         if eng.zero:
             for a, b, go in eng._owned_segments(e.offset, e.offset + e.numel):
                 pieces.append({**base, "kind": "flat", "e0": a - e.offset, "e1": b - e.offset,
@@ -117,6 +126,9 @@ def _piece_boxes(p: dict) -> list[tuple]:
     ro, co = p["row_off"], p["col_off"]
     if p["kind"] == "rows":
         return [(ro + p["r0"], ro + p["r1"], co, co + p["cols"], p["r0"], 0, None)]
+    if p.get("t"):   # stored transposed: stored rows are logical columns
+        return [(ro + c0, ro + c1, co + r0, co + r1, r0, c0, fs) for r0, r1, c0, c1, fs in
+                _flat_boxes(p["e0"], p["e1"], p["cols"])]
     return [(ro + r0, ro + r1, co + c0, co + c1, r0, c0, fs) for r0, r1, c0, c1, fs in
             _flat_boxes(p["e0"], p["e1"], p["cols"])]
 
@@ -195,9 +207,15 @@ def _needed_boxes(eng, e) -> list[tuple]:
     rows, cols, ro, co = _local_geom(eng, e.name)
     if eng.zero:
         out = []
+        t = _stored_t(eng, e.name)
+        sc = rows if t else cols   # columns of the stored geometry
         for a, b, go in eng._owned_segments(e.offset, e.offset + e.numel):
-            for r0, r1, c0, c1, fs in _flat_boxes(a - e.offset, b - e.offset, cols):
-                out.append((ro + r0, ro + r1, co + c0, co + c1, ("flat", go + (fs - (a - e.offset)), r0, c0, cols)))
+            for r0, r1, c0, c1, fs in _flat_boxes(a - e.offset, b - e.offset, sc):
+                dest = ("flatT" if t else "flat", go + (fs - (a - e.offset)), r0, c0, sc)
+                if t:
+                    out.append((ro + c0, ro + c1, co + r0, co + r1, dest))
+                else:
+                    out.append((ro + r0, ro + r1, co + c0, co + c1, dest))
         return out
     if eng.fsdp:
         own = rows // eng.mesh.dp
@@ -217,6 +235,15 @@ def _fill(eng, target: torch.Tensor, e, sources, reader: _Reader) -> int:
             blk = read(a, b, c, d).to(device=target.device, dtype=target.dtype)  # [b-a, d-c]
             if dest[0] == "rows":  # the stored 2-D view (FSDP: its row shard) starts at global row R0
                 eng.logical_view(target, e)[(a - R0):(b - R0), (c - C0):(d - C0)].copy_(blk)
+            elif dest[0] == "flatT":
+                # stored transposed: logical rows [a, b) are stored columns, logical columns [c, d) stored rows
+                _, start, lr0, lc0, cols = dest
+                base = start + (c - C0) * cols + (a - R0)
+                bt = blk.t()
+                if d - c == 1:
+                    target[base:base + (b - a)].copy_(bt.reshape(-1))
+                else:
+                    target[base:base + (d - c - 1) * cols + (b - a)].as_strided((d - c, b - a), (cols, 1)).copy_(bt)
             else:
                 _, start, lr0, lc0, cols = dest
                 # box rows are local rows lr0.. of the flat segment; flat index of (row, col) relative to
@@ -242,6 +269,16 @@ def _sharded_sources(path: str, meta: dict, reader: _Reader) -> dict:
                 if p["kind"] == "rows":
                     def read(a, b, c, d, p=p, R0=R0, C0=C0, fname=fname):
                         return reader.slice(fname, p["key"], (slice(a - R0, b - R0), slice(c - C0, d - C0)))
+                elif p.get("t"):
+                    def read(a, b, c, d, p=p, R0=R0, C0=C0, fs=fs, fname=fname):
+                        # stored transposed: logical rows [a, b) = stored columns, logical columns [c, d) = stored
+                        # rows; read the stored block, return it transposed
+                        cols = p["cols"]
+                        first = fs - p["e0"] + (c - C0) * cols + (a - R0)
+                        if d - c == 1:
+                            return reader.slice(fname, p["key"], slice(first, first + (b - a))).view(1, b - a).t()
+                        span = reader.slice(fname, p["key"], slice(first, first + (d - c - 1) * cols + (b - a)))
+                        return span.as_strided((d - c, b - a), (cols, 1)).t()
                 else:
                     def read(a, b, c, d, p=p, R0=R0, C0=C0, lr0=lr0, lc0=lc0, fs=fs, fname=fname):
                         cols = p["cols"]

@@ -78,6 +78,9 @@ class TrainConfig:
     # transposed map); "auto" = nn_w2t where the engine supports it (GPU, bf16, 256x256 8-phase shapes without split-K,
     # no TP / SP / FSDP / recompute, fused SGD / AdamW on split masters or stored gradients)
     wgrad_layout: str = "auto"
+    # W2's storage in the row-major layer: "auto" (transposed W2ᵀ [F, D] with the nn_w2t weight-gradient mode),
+    # "rowmajor", or "transposed" (any weight-gradient layout; no TP / SP / FSDP; checkpoints stay logical [D, F])
+    w2_storage: str = "auto"
     wgrad_stream: bool = False       # single device, fused optimizer: weight-gradient GEMMs on a second
                                      # stream, concurrent with the dgrad chain (CUs shared; epilogues overlap)
     wgrad_stream_max_tpc: float = 4.0  # wgrad_stream only while a weight gradient has <= this many 256x256 tiles

@@ -312,3 +312,39 @@ def test_force_tp_comm_runs_tp_collectives_at_world1(sp, want, free_port):
     r = _run(cfg, 4, 1, free_port, rec=True, count_collectives=True, force_dist=True)
     assert r["collectives_per_step"]["tp"] == want
     _close(r["params"], _oracle(cfg, 1))
+
+
+@pytest.mark.parametrize("method,n", [(1, 1), (2, 2), (6, 2), (6, 4)], ids=["single", "ddp2", "zero2", "zero4"])
+def test_w2_transposed_storage_matches_rowmajor(method, n, free_port):
+    """W2 stored as W2ᵀ [F, D] in the row-major layer (``w2_storage``; the NN weight-gradient layout's storage on the
+    GPU): the dgrad runs NT, dW2 writes through the transposed output map, and ZeRO shards / buckets the transposed
+    flat entry -- the logical parameters equal the row-major run's."""
+    kw = dict(D=64, F=256, L=3, steps=4, optimizer="adam", lr=1e-3)
+    a = _run(_cfg(w2_storage="rowmajor", **kw), method, n, free_port, rec=True)
+    b = _run(_cfg(w2_storage="transposed", **kw), method, n, free_port + 1, rec=True)
+    assert b["layout"]["w2t"] and not a["layout"]["w2t"]
+    # 4 gloo ranks: W2's elements sit in other ring chunks of the flat buckets, so their sums run in another order
+    # (a few elements differ in the last bits; 2-term sums are order-free)
+    _close(b["params"], a["params"], rtol=1e-6, atol=1e-8 if n <= 2 else 1e-6)
+
+
+@pytest.mark.parametrize("fmt", ["sharded", "consolidated"])
+def test_w2_transposed_storage_checkpoints_cross(fmt, tmp_path, free_port):
+    """ZeRO-2 checkpoints written with W2 stored transposed resume with it stored row-major and vice versa, on another
+    world size (the flat ZeRO pieces of W2ᵀ map back to logical [D, F] boxes); the continued runs equal the
+    uninterrupted one."""
+    kw = dict(D=64, F=256, L=2, steps=4, optimizer="adam", lr=1e-3)
+    rm, tr = _cfg(w2_storage="rowmajor", **kw), _cfg(w2_storage="transposed", **kw)
+    full = _run(rm, 6, 2, free_port)
+    port = free_port + 1
+    for i, (src, dst) in enumerate(((tr, rm), (rm, tr), (tr, tr))):
+        ck = str(tmp_path / f"ck{i}")
+        _run(src, 6, 4, port, ckpt_dir=ck, stop_after=1, ckpt_format=fmt)     # 4 ranks: one step each
+        saved, _ = load_logical(ck)
+        r = _run(dst, 6, 2, port + 1, rec=True, resume=ck, stop_after=1)   # load only: equals the saved state
+        _close(r["params"], saved["params"], rtol=0, atol=0)
+        port += 2
+    # a 2-rank uninterrupted run vs its first step with W2 transposed + the rest resumed with W2 row-major
+    ck = str(tmp_path / "ck_cont")
+    _run(tr, 6, 2, port, ckpt_dir=ck, stop_after=1, ckpt_format=fmt)
+    _close(_run(rm, 6, 2, port + 1, resume=ck), full, rtol=1e-6, atol=1e-8)

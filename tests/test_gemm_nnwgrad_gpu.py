@@ -126,7 +126,7 @@ def test_transposed_outputs_reject_bad_shapes():
     with pytest.raises(ValueError):
         gemm(b.t().contiguous(), a[:192], "nn", out_t=True)
     with pytest.raises(ValueError):
-        gemm(a, a, "tn", out_t=True, epi="sgd_split")    # transposed fused optimizer: NN only
+        gemm(a, a, "nt", out_t=True, epi="sgd_split")    # transposed fused optimizer: NN / TN only
 
 
 @pytest.mark.parametrize("variant", ["fused_serial", "fused_wgrad_stream", "grads_fp32", "grads_bf16",
