@@ -214,9 +214,36 @@ def epilogue_pitch():
         print(f"pitch {N + pad:6d}: store {s0:7.1f} us, fused SGD {s1:7.1f} us, epilogue {s1 - s0:6.1f} us", flush=True)
 
 
+
+
+def raster_t():
+    """The step's NN-layout GEMMs by raster band height group_m: the transposed-map fused SGD weight gradient
+    (M = 4096, N = 16384, K = 8192) and the NN stores with a transposed copy (fwd-2 / dx shape [8192, 4096], K = 16384)."""
+    g = torch.Generator().manual_seed(5)
+    bf = torch.bfloat16
+    T, D, F = 8192, 4096, 16384
+    xT = torch.randn(D, T, generator=g).to(bf).cuda()
+    da = torch.randn(T, F, generator=g).to(bf).cuda()
+    hi, lo = split_master((torch.randn(F, D, generator=g) * 0.02).cuda())
+    a = torch.randn(T, F, generator=g).to(bf).cuda()
+    w2t = (torch.randn(F, D, generator=g) * 0.02).to(bf).cuda()
+    y = torch.empty(T, D, dtype=bf, device="cuda")
+    yT = torch.empty(D, T, dtype=bf, device="cuda")
+    for gm in (1, 2, 4, 8):
+        r0, r1 = [], []
+        for _ in range(5):
+            r0.append(timeit(lambda: gemm(xT, da, "nn", out=lo, epi="sgd_split", lr=1e-9, aux_out=hi, out_t=True,
+                                          group_m=gm), 10))
+            r1.append(timeit(lambda: gemm(a, w2t, "nn", out=y, aux_t=yT, group_m=gm), 10))
+        print(f"group_m {gm}: dW1 NN-T fused SGD {statistics.median(r0):7.1f} us, y NN + copy {statistics.median(r1):7.1f} us",
+              flush=True)
+
+
 if __name__ == "__main__":
     if "--operand_order" in sys.argv:   # python scripts/bench_nn_wgrad.py --operand_order
         operand_order()
+    elif "--raster_t" in sys.argv:
+        raster_t()
     elif "--epilogue_pitch" in sys.argv:
         epilogue_pitch()
     elif "--epilogue_raster" in sys.argv:
