@@ -245,7 +245,7 @@ class FFNTrainer:
             raise ValueError(f"unknown w2_storage {cfg.w2_storage!r}")
         self.w2s = not self.tmode and (cfg.w2_storage == "transposed" or
                                        (cfg.w2_storage == "auto" and self.wgrad_nn and mode == "nn_w2t"))
-        if self.w2s and (self.tp_comm or self.sp or self.fsdp or self.pair_wgrads):
+        if self.w2s and (self.tp_comm or self.sp or self.pair_wgrads):
             raise ValueError("w2_storage transposed: row-major data-parallel / single-device layers only")
         self.w2t = self.tmode or self.w2s
 
@@ -450,7 +450,7 @@ class FFNTrainer:
 
     def _wgrad_nn_supported(self) -> bool:
         """Whether the weight gradients run in the NN layout (``cfg.wgrad_layout``; models/ffn.NNWgrad): GPU, bf16, the
-        plain row-major layer (no TP / SP / FSDP / transposed-activation mode / recompute / grouped pair / TP chunks),
+        plain row-major layer (no TP / SP / transposed-activation mode / recompute / grouped pair / TP chunks),
         256x256 8-phase shapes, and a fused optimizer only on split masters (SGD / AdamW; stored gradients: any)."""
         cfg = self.cfg
         if cfg.wgrad_layout not in ("auto", "tn", "nn", "nn_w1", "nn_w2t"):
@@ -463,7 +463,7 @@ class FFNTrainer:
         why = []
         if self.device.type != "cuda" or self.cd != torch.bfloat16:
             why.append("GPU bf16 only")
-        if self.tp_comm or self.sp or self.fsdp or self.tmode or self.pair_wgrads:
+        if self.tp_comm or self.sp or self.tmode or self.pair_wgrads:
             why.append("row-major data-parallel / single-device layers only")
         if cfg.recompute != "none":
             why.append("kept activations only")
@@ -810,12 +810,12 @@ class FFNTrainer:
             for name in ("w1", "w2"):
                 e = self.entry[(l, name)]
                 mv = self.master_slice(e.offset, e.offset + e.numel).view(e.shape) if per_entry else self._view(src, e)
-                if self.w2t and name == "w2":
-                    mv = mv.t()   # logical [D, F_loc] from the stored W2ᵀ
-                if self.fsdp:
+                if self.fsdp:   # row shards of the STORED matrix (W2ᵀ: rows are F)
                     full = torch.empty(self.entry[(l, name)].full_shape, dtype=torch.float32, device=self.device)
                     comm.all_gather_into(full, mv.contiguous(), self.mesh.group("dp_ag"), async_op=False)
                     mv = full
+                if self.w2t and name == "w2":
+                    mv = mv.t()   # logical [D, F_loc] from the stored W2ᵀ
                 p[name] = mv
             if self.gated:
                 w1, w3 = deinterleave_w13(p["w1"])

@@ -113,6 +113,10 @@ def _owned_pieces(eng) -> list[dict]:
             for a, b, go in eng._owned_segments(e.offset, e.offset + e.numel):
                 pieces.append({**base, "kind": "flat", "e0": a - e.offset, "e1": b - e.offset,
                                "src": go})  # src: offset in the stored shard buffer
+        elif eng.fsdp and _stored_t(eng, e.name):
+            # FSDP row shards of the stored W2ᵀ are logical COLUMN ranges of W2 [D, F]
+            own = cols // d
+            pieces.append({**base, "kind": "cols", "c0": dr * own, "c1": (dr + 1) * own, "src": e.offset})
         elif eng.fsdp:
             own = rows // d
             pieces.append({**base, "kind": "rows", "r0": dr * own, "r1": (dr + 1) * own, "src": e.offset})
@@ -126,6 +130,8 @@ def _piece_boxes(p: dict) -> list[tuple]:
     ro, co = p["row_off"], p["col_off"]
     if p["kind"] == "rows":
         return [(ro + p["r0"], ro + p["r1"], co, co + p["cols"], p["r0"], 0, None)]
+    if p["kind"] == "cols":
+        return [(ro, ro + p["rows"], co + p["c0"], co + p["c1"], 0, p["c0"], None)]
     if p.get("t"):   # stored transposed: stored rows are logical columns
         return [(ro + c0, ro + c1, co + r0, co + r1, r0, c0, fs) for r0, r1, c0, c1, fs in
                 _flat_boxes(p["e0"], p["e1"], p["cols"])]
@@ -163,6 +169,8 @@ def save_checkpoint(eng, path: str, step: int, fmt: str = "consolidated", meta: 
                 key = f"{bname}/{p['layer']}/{p['name']}/{i}"
                 if p["kind"] == "flat":
                     t = flat[p["src"]:p["src"] + (p["e1"] - p["e0"])]
+                elif p["kind"] == "cols":   # FSDP shard of a stored W2ᵀ: the logical column block, whole
+                    t = eng.logical_view(flat, eng.entry[(p["layer"], p["name"])])
                 else:
                     e = eng.entry[(p["layer"], p["name"])]
                     own = eng.logical_view(flat, e)  # the stored 2-D tensor, [out, in] (FSDP: its row shard)
@@ -217,6 +225,10 @@ def _needed_boxes(eng, e) -> list[tuple]:
                 else:
                     out.append((ro + r0, ro + r1, co + c0, co + c1, dest))
         return out
+    if eng.fsdp and _stored_t(eng, e.name):   # stored W2ᵀ row shard = logical column block
+        own = cols // eng.mesh.dp
+        c0 = eng.mesh.dp_rank * own
+        return [(ro, ro + rows, co + c0, co + c0 + own, ("cols", c0))]
     if eng.fsdp:
         own = rows // eng.mesh.dp
         r0 = eng.mesh.dp_rank * own
@@ -233,7 +245,7 @@ def _fill(eng, target: torch.Tensor, e, sources, reader: _Reader) -> int:
             if a >= b or c >= d:
                 continue
             blk = read(a, b, c, d).to(device=target.device, dtype=target.dtype)  # [b-a, d-c]
-            if dest[0] == "rows":  # the stored 2-D view (FSDP: its row shard) starts at global row R0
+            if dest[0] in ("rows", "cols"):  # the stored 2-D view (FSDP: its shard) starts at global (R0, C0)
                 eng.logical_view(target, e)[(a - R0):(b - R0), (c - C0):(d - C0)].copy_(blk)
             elif dest[0] == "flatT":
                 # stored transposed: logical rows [a, b) are stored columns, logical columns [c, d) stored rows
@@ -266,7 +278,7 @@ def _sharded_sources(path: str, meta: dict, reader: _Reader) -> dict:
         fname = f"rank{r}.safetensors"
         for p in idx["pieces"]:
             for R0, R1, C0, C1, lr0, lc0, fs in _piece_boxes(p):
-                if p["kind"] == "rows":
+                if p["kind"] in ("rows", "cols"):
                     def read(a, b, c, d, p=p, R0=R0, C0=C0, fname=fname):
                         return reader.slice(fname, p["key"], (slice(a - R0, b - R0), slice(c - C0, d - C0)))
                 elif p.get("t"):

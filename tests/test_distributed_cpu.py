@@ -314,7 +314,8 @@ def test_force_tp_comm_runs_tp_collectives_at_world1(sp, want, free_port):
     _close(r["params"], _oracle(cfg, 1))
 
 
-@pytest.mark.parametrize("method,n", [(1, 1), (2, 2), (6, 2), (6, 4)], ids=["single", "ddp2", "zero2", "zero4"])
+@pytest.mark.parametrize("method,n", [(1, 1), (2, 2), (6, 2), (6, 4), (3, 2), (3, 4)],
+                         ids=["single", "ddp2", "zero2", "zero4", "fsdp2", "fsdp4"])
 def test_w2_transposed_storage_matches_rowmajor(method, n, free_port):
     """W2 stored as W2ᵀ [F, D] in the row-major layer (``w2_storage``; the NN weight-gradient layout's storage on the
     GPU): the dgrad runs NT, dW2 writes through the transposed output map, and ZeRO shards / buckets the transposed
@@ -323,9 +324,22 @@ def test_w2_transposed_storage_matches_rowmajor(method, n, free_port):
     a = _run(_cfg(w2_storage="rowmajor", **kw), method, n, free_port, rec=True)
     b = _run(_cfg(w2_storage="transposed", **kw), method, n, free_port + 1, rec=True)
     assert b["layout"]["w2t"] and not a["layout"]["w2t"]
-    # 4 gloo ranks: W2's elements sit in other ring chunks of the flat buckets, so their sums run in another order
-    # (a few elements differ in the last bits; 2-term sums are order-free)
+    # 4 gloo ranks: W2's elements sit in other ring chunks of the flat buckets / shards, so their sums run in another
+    # order (a few elements differ in the last bits; 2-term sums are order-free)
     _close(b["params"], a["params"], rtol=1e-6, atol=1e-8 if n <= 2 else 1e-6)
+
+
+@pytest.mark.parametrize("src,dst", [((3, "transposed"), (6, "rowmajor")), ((6, "transposed"), (3, "transposed")),
+                                     ((3, "rowmajor"), (3, "transposed"))], ids=["fsdpT-zero", "zeroT-fsdpT", "fsdp-fsdpT"])
+def test_w2_transposed_storage_fsdp_checkpoints(src, dst, tmp_path, free_port):
+    """FSDP shards of a stored W2ᵀ are logical column blocks (``cols`` pieces): sharded checkpoints cross between
+    FSDP / ZeRO, storages and world sizes and load back exactly."""
+    kw = dict(D=64, F=256, L=2, steps=4, optimizer="adam", lr=1e-3)
+    ck = str(tmp_path / "ck")
+    _run(_cfg(w2_storage=src[1], **kw), src[0], 4, free_port, ckpt_dir=ck, stop_after=1, ckpt_format="sharded")
+    saved, _ = load_logical(ck)
+    r = _run(_cfg(w2_storage=dst[1], **kw), dst[0], 2, free_port + 1, rec=True, resume=ck, stop_after=1)
+    _close(r["params"], saved["params"], rtol=0, atol=0)
 
 
 @pytest.mark.parametrize("fmt", ["sharded", "consolidated"])

@@ -102,7 +102,7 @@ def test_tp_transposed_layout_two_ranks_and_checkpoint_crossing(free_port, tmp_p
 
 def test_nn_weight_gradient_layout_two_ranks_and_checkpoint_crossing(free_port, tmp_path):
     """The NN weight-gradient layout (nn_w2t: W2 stored transposed, transposed xᵀ / dyᵀ copies, stored gradients
-    through the transposed map) on 2 real DDP / ZeRO-2 ranks: bitwise the TN layout's masters; a sharded ZeRO
+    through the transposed map) on 2 real DDP / ZeRO-2 / FSDP ranks: bitwise the TN layout's masters; a sharded ZeRO
     checkpoint written in one layout resumes in the other (both directions).  Shapes large enough that no GEMM of the
     layer takes split-K (the engine's condition for the NN layout)."""
     base = dict(dtype="bf16", grad_dtype="bf16", lr=1e-3)
@@ -111,7 +111,7 @@ def test_nn_weight_gradient_layout_two_ranks_and_checkpoint_crossing(free_port, 
     tn = _cfg(D, F, L, T, wgrad_layout="tn", **base)
     port = free_port
     ref = {}
-    for method in (2, 6):                          # DDP, ZeRO-2
+    for method in (2, 6, 3):                       # DDP, ZeRO-2, FSDP
         ra = _run(nn, method, 2, port, record=True)
         rb = _run(tn, method, 2, port + 1, record=True)
         port += 2
