@@ -177,7 +177,8 @@ def parse(argv=None):
                    help="capture the whole step (data + fwd + bwd + fused SGD) in a HIP graph (N=1 path)")
     p.add_argument("--side_opt", type=int, default=0,
                    help="N=1: store wgrads and run SGD on a side stream over this many workgroups (0 = fuse the "
-                        "update into the wgrad GEMM epilogue)")
+                        "update into the wgrad GEMM epilogue; -1 = each weight's flat update, any optimizer, on the "
+                        "side stream with the whole chip)")
     p.add_argument("--phases", action="store_true",
                    help="also report per-phase GPU time (forward / backward / optimizer tail) from HIP events")
     p.add_argument("--wgrad_layout", choices=["auto", "tn", "nn", "nn_w1", "nn_w2t"], default="auto",

@@ -211,11 +211,16 @@ class FFNTrainer:
         # stream updates the weight while the next GEMMs run; the forward waits per weight
         # (SGD only: a side-stream AdamW on the split master was measured 63 % slower on config 5 and removed, round 5,
         # profiles/r5/adamw_fused_vs_side_r5.txt)
-        self.side_opt = (no_coll and cfg.side_optimizer > 0 and cfg.optimizer == "sgd" and dev.type == "cuda")
+        # side_optimizer < 0: the weight gradients are stored and each weight's flat update (SGD / AdamW, split masters)
+        # runs on the side stream with the whole chip, overlapping the next GEMMs -- the schedule FSDP at dp = 1 runs,
+        # which beats the fused AdamW epilogue (24 B/parameter inside the GEMM) on config 5
+        self.side_opt = no_coll and dev.type == "cuda" and (
+            (cfg.side_optimizer > 0 and cfg.optimizer == "sgd") or cfg.side_optimizer < 0)
         # Split master (bf16 SGD): the fp32 master is the bf16 working copy (hi) plus an int16 residual plane (lo),
         # bitwise the same fp32 values (ops/master.py).  4 B/param of weight state instead of 6 B, and every update
         # (fused wgrad epilogue or flat kernel) reads 4 B and writes 4 B per parameter instead of 4 B + 6 B.
-        self.split = cfg.master == "split" and self.cd == torch.bfloat16 and not self.side_opt
+        self.split = (cfg.master == "split" and self.cd == torch.bfloat16
+                      and not (self.side_opt and cfg.side_optimizer > 0))   # the capped SGD kernel: fp32 masters
         if cfg.master not in ("split", "fp32"):
             raise ValueError(f"unknown master format {cfg.master!r}")
         self.fused_opt = cfg.fused_optimizer and no_coll and not self.side_opt
@@ -882,9 +887,12 @@ class FFNTrainer:
             st = self.opt_stream_side
             st.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(st):
-                copy = None if self.shared_copy else self.copy[s_:e_]
-                sgd_step_(self._master[s_:e_], self.grads[s_:e_], self.cfg.lr, copy=copy,
-                          max_blocks=self.cfg.side_optimizer)
+                if self.cfg.side_optimizer < 0:
+                    self._opt(s_, e_)             # whole chip, any optimizer, split or fp32 masters
+                else:
+                    copy = None if self.shared_copy else self.copy[s_:e_]
+                    sgd_step_(self._master[s_:e_], self.grads[s_:e_], self.cfg.lr, copy=copy,
+                              max_blocks=self.cfg.side_optimizer)
                 ev = torch.cuda.Event()
                 ev.record(st)
             self.opt_done[(l, name)] = ev

@@ -91,7 +91,8 @@ class TrainConfig:
                                      # (8 -- the launcher picks the makespan-optimal count under it)
     fused_optimizer: bool = True     # fuse SGD/Adam into the wgrad GEMM epilogue when no grad collective
     side_optimizer: int = 0          # >0 (no grad collective, SGD): wgrad GEMMs store grads and a side stream
-                                     # applies SGD on this many workgroups, overlapped with the next GEMMs
+                                     # applies SGD on this many workgroups, overlapped with the next GEMMs;
+                                     # <0: the same with the whole chip, any optimizer, split masters
     force_comm: bool = False         # run the DDP/FSDP collective path even at dp=1 (single-GPU RCCL check)
     fsdp_alias: bool = True          # FSDP at dp = 1: gathers / gradient writes alias the full buffers (size-1
                                      # collectives move nothing); False: the dp > 1 rings + real copying collectives
