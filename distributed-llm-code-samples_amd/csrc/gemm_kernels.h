@@ -45,6 +45,10 @@
 #ifndef DLLM_F32_256
 #define DLLM_F32_256 1
 #endif
+// transposed-map fused AdamW (EPI_ADAMS_T): persistent blocks (1) or one tile per block (0, as the other AdamW epilogues)
+#ifndef DLLM_ADAMS_T_PERS
+#define DLLM_ADAMS_T_PERS 0
+#endif
 
 #include "common.h"
 
@@ -2128,7 +2132,7 @@ static hipError_t launch_splitk(const GemmArgs& a, int out_dt, float* ws, hipStr
 template <int L, int E, typename OutT, int ACT>
 constexpr bool persistent_kernel() {
   constexpr bool bf = std::is_same<OutT, uint16_t>::value;
-  if constexpr (E == EPI_ADAMS_T) return false;   // fused AdamW: one tile per block (see above)
+  if constexpr (E == EPI_ADAMS_T) return DLLM_ADAMS_T_PERS;   // fused AdamW: one tile per block (see above)
   if constexpr (E == EPI_STORE_DT || E == EPI_STORE_T || E == EPI_SGDS_T) return true;
   if constexpr (L == L_NN && E == EPI_SGDS) return true;   // the NN weight-gradient layout (dispatch_x)
   // gated (SwiGLU) stacks: the GLU forward / DGLU dgrad with a compile-time activation (round 3)
