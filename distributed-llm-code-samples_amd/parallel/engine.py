@@ -212,8 +212,9 @@ class FFNTrainer:
         # (SGD only: a side-stream AdamW on the split master was measured 63 % slower on config 5 and removed, round 5,
         # profiles/r5/adamw_fused_vs_side_r5.txt)
         # side_optimizer < 0: the weight gradients are stored and each weight's flat update (SGD / AdamW, split masters)
-        # runs on the side stream with the whole chip, overlapping the next GEMMs -- the schedule FSDP at dp = 1 runs,
-        # which beats the fused AdamW epilogue (24 B/parameter inside the GEMM) on config 5
+        # runs on the side stream with the whole chip, overlapping the next GEMMs -- the schedule FSDP at dp = 1 runs.
+        # An option: it measured slower than the fused epilogues (config 5 AdamW 185.8-187.2 vs 181.4-182.0 ms, the
+        # flagship 29.45 vs 28.2 ms; profiles/r5/side_opt_whole_chip_r5.txt)
         self.side_opt = no_coll and dev.type == "cuda" and (
             (cfg.side_optimizer > 0 and cfg.optimizer == "sgd") or cfg.side_optimizer < 0)
         # Split master (bf16 SGD): the fp32 master is the bf16 working copy (hi) plus an int16 residual plane (lo),
