@@ -1,3 +1,3 @@
 #!/bin/bash
 source scripts/gpu_steps.sh
-step raster_t 300 python -u scripts/bench_nn_wgrad.py --raster_t
+step probe_div 300 python -u scripts/probe_divergence.py
