@@ -228,7 +228,9 @@ def parse(argv=None):
                    help="fp32 master weights of a bf16 run: split (bf16 working copy + int16 residual, exactly the "
                         "fp32 master, 4 B/param) or a separate fp32 buffer (6 B/param with the copy)")
     p.add_argument("--group_m_nt", type=int, default=4,
-                   help="tiles per raster band of the forward (NT) GEMMs (backward GEMMs: 4)")
+                   help="tiles per raster band of the NT-layout GEMMs")
+    p.add_argument("--group_m_nn", type=int, default=8,
+                   help="tiles per raster band of the NN-layout GEMMs (TN: 4)")
     p.add_argument("--dist_first", action="store_true",
                    help="diagnostic: create the process group before the N=1 headline (as N>1 runs must)")
     p.add_argument("--force_comm", action="store_true",
@@ -577,9 +579,10 @@ def main(argv=None) -> int:
 
         set_bf16_variant(a.gemm_variant)
     if not cpu:
-        from dllm.ops.gemm import set_group_m_nt, set_pair_wgrads
+        from dllm.ops.gemm import set_group_m_nn, set_group_m_nt, set_pair_wgrads
 
         set_group_m_nt(a.group_m_nt)
+        set_group_m_nn(a.group_m_nn)
         set_pair_wgrads(not a.no_pair_wgrads)
     ffn = a.ffn_dim or (a.mp_ffn_dim if a.method == "tp" else 0)
     model = ModelConfig(model_size=a.model_size, ffn_dim=ffn, layers=a.layers, act=a.act, gated=a.gated)
