@@ -230,7 +230,9 @@ def parse(argv=None):
     p.add_argument("--group_m_nt", type=int, default=4,
                    help="tiles per raster band of the NT-layout GEMMs")
     p.add_argument("--group_m_nn", type=int, default=8,
-                   help="tiles per raster band of the NN-layout GEMMs (TN: 4)")
+                   help="tiles per raster band of the NN-layout GEMMs")
+    p.add_argument("--group_m_tn", type=int, default=4,
+                   help="tiles per raster band of the TN-layout GEMMs")
     p.add_argument("--dist_first", action="store_true",
                    help="diagnostic: create the process group before the N=1 headline (as N>1 runs must)")
     p.add_argument("--force_comm", action="store_true",
@@ -579,10 +581,11 @@ def main(argv=None) -> int:
 
         set_bf16_variant(a.gemm_variant)
     if not cpu:
-        from dllm.ops.gemm import set_group_m_nn, set_group_m_nt, set_pair_wgrads
+        from dllm.ops.gemm import set_group_m_nn, set_group_m_nt, set_group_m_tn, set_pair_wgrads
 
         set_group_m_nt(a.group_m_nt)
         set_group_m_nn(a.group_m_nn)
+        set_group_m_tn(a.group_m_tn)
         set_pair_wgrads(not a.no_pair_wgrads)
     ffn = a.ffn_dim or (a.mp_ffn_dim if a.method == "tp" else 0)
     model = ModelConfig(model_size=a.model_size, ffn_dim=ffn, layers=a.layers, act=a.act, gated=a.gated)

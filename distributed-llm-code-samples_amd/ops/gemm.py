@@ -261,7 +261,7 @@ _VARIANT = {"name": "auto"}
 # group_m_nn: 8 -- the NN-layout GEMMs of the finite-data step (NN stores with transposed copies, transposed-map weight
 # gradients) ran 34.13-34.18 ms against 34.26-34.35 at 4 and 34.97-35.01 at 16 (5 interleaved pairs,
 # profiles/r5/group_m_nn_finite_r5.txt)
-_POLICY = {"tpb": 8, "min_bpc": 1, "group_m_nt": 4, "group_m_nn": 8}  # tpb: the cap; the library picks the makespan-optimal tiles per block
+_POLICY = {"tpb": 8, "min_bpc": 1, "group_m_nt": 4, "group_m_nn": 8, "group_m_tn": 4}  # tpb: the cap; the library picks the makespan-optimal tiles per block
 # split-K fp32 partial workspaces, cached per (device, stream): a GEMM only ever reuses its own stream's
 # buffer, so stream order serialises the reuse
 _WS: dict = {}
@@ -290,7 +290,8 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
     if out_t or aux_t is not None:
         _check_transposed(a, layout, epi, M, N, K, out_t, aux_t, beta)
     if group_m is None:   # raster band height: the layout's policy (profiles/r3/group_m_sweep_r3.txt)
-        group_m = _POLICY["group_m_nt"] if layout == "nt" else _POLICY["group_m_nn"] if layout == "nn" else 4
+        group_m = _POLICY["group_m_nt"] if layout == "nt" else _POLICY["group_m_nn"] if layout == "nn" else \
+            _POLICY["group_m_tn"]
     if a.dtype != b.dtype:
         raise TypeError(f"gemm operands differ in dtype: {a.dtype} vs {b.dtype}")
     nout = out_cols(N, epi)
@@ -599,6 +600,13 @@ def set_group_m_nn(n: int) -> int:
     """Tiles per raster band of the NN-layout GEMMs (dgrad / NN weight gradients / NN stores); returns the previous."""
     old = _POLICY["group_m_nn"]
     _POLICY["group_m_nn"] = max(1, int(n))
+    return old
+
+
+def set_group_m_tn(n: int) -> int:
+    """Tiles per raster band of the TN-layout GEMMs (weight gradients, the TP shard's forward); returns the previous."""
+    old = _POLICY["group_m_tn"]
+    _POLICY["group_m_tn"] = max(1, int(n))
     return old
 
 
