@@ -591,6 +591,11 @@ def main(argv=None) -> int:
     model = ModelConfig(model_size=a.model_size, ffn_dim=ffn, layers=a.layers, act=a.act, gated=a.gated)
     head = run_method(a, a.method, n, world, dev, a.steps, a.warmup, a.force_comm, model,
                       observe_steps=a.observe_steps, headline=True)
+    head_policy = None
+    if not cpu:
+        from dllm.ops.gemm import _POLICY
+
+        head_policy = dict(_POLICY)
     ref_init = None
     if not cpu and not a.no_reference_init and a.init_scale in ("auto", "fan_in") and not model.gated:
         # the same headline run with the reference's 2e-2 init (diverges after the first update; see --init_scale)
@@ -632,6 +637,8 @@ def main(argv=None) -> int:
             "pair_wgrads": head.get("pair_wgrads", False), "tp_transposed": head.get("tp_transposed", False),
             "wgrad_nn": head.get("wgrad_nn", False), "wgrad_nn_w2": head.get("wgrad_nn_w2", False),
         }
+        if head_policy is not None:
+            rec["gemm_policy"] = head_policy   # raster bands, tiles per block, blocks per CU of the headline's GEMMs
         if ref_init is not None:
             rec["reference_init"] = ref_init
         for k in ("comm", "phase_ms_per_step", "queues", "collectives_elided"):
