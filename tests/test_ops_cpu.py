@@ -210,3 +210,19 @@ def test_wgrad_layout_nn_needs_gpu():
         else:
             with pytest.raises(ValueError, match="wgrad_layout nn"):
                 FFNTrainer(cfg, Mesh(), torch.device("cpu"))
+
+
+def test_raster_band_policies_round_trip():
+    """Per-layout raster bands (ops.gemm policy): each setter returns the previous value and clamps to >= 1; the
+    default bands are NT 4, NN 8 (profiles/r5/group_m_nn_finite_r5.txt), TN 4."""
+    from dllm.ops.gemm import _POLICY, set_group_m_nn, set_group_m_nt, set_group_m_tn
+
+    assert (_POLICY["group_m_nt"], _POLICY["group_m_nn"], _POLICY["group_m_tn"]) == (4, 8, 4)
+    for setter, key in ((set_group_m_nt, "group_m_nt"), (set_group_m_nn, "group_m_nn"), (set_group_m_tn, "group_m_tn")):
+        old = setter(0)
+        try:
+            assert _POLICY[key] == 1
+            assert setter(16) == 1 and _POLICY[key] == 16
+        finally:
+            setter(old)
+        assert _POLICY[key] == old
