@@ -534,6 +534,17 @@ def _run_on_mesh(a, method, cfg, mesh, n, world, dev, steps, warmup, force_comm,
     return rec
 
 
+def data_note(init, finite: bool, overlap: bool = False) -> str:
+    """The JSON ``data`` string.  Whether the data stayed finite is read from the run (``finite``: every weight of the
+    working copy after the timed steps), never assumed: ``--init_scale 0.02`` overflows the flagship stack."""
+    return ("synthetic (device Philox N(0,1) x, 0.1*N(0,1) dloss/dx, drawn every step" +
+            (", the next batch on a side stream under the backward" if overlap else "") +
+            f"; random-init weights, std {init}: " +
+            ("finite data throughout" if finite else
+             "NON-FINITE: the weights overflowed to inf / NaN during the run, the GEMMs ran on degenerate data") +
+            ", see reference_init)")
+
+
 SIDE_KEYS = ("value", "ms_per_step", "tflops_per_gpu", "peak_hbm_gib", "parallelism", "model", "global_batch",
              "steps", "warmup", "warmup_ms", "timed_ms", "finite", "init", "state_gib", "comm", "queues", "comm_sizes",
              "pair_wgrads", "tp_transposed", "wgrad_nn", "wgrad_nn_w2", "tp_allreduce_choice")
@@ -623,15 +634,13 @@ def main(argv=None) -> int:
             "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "default"),
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": head["ms_per_step"], "higher_is_better": True,
             "scaling": "strong" if a.method == "tp" else "weak", "vs_baseline": None, "dtype": a.dtype,
-            "data": "synthetic (device Philox N(0,1) x, 0.1*N(0,1) dloss/dx, drawn every step" +
-                    (", the next batch on a side stream under the backward" if a.data_overlap else "") +
-                    f"; random-init weights, std {head.get('init')}: finite data throughout, see reference_init)",
+            "data": data_note(head.get("init"), head["finite"], a.data_overlap), "finite": head["finite"],
             "config": {"model": head["model"], "global_batch": head["global_batch"], "seq_len": a.seq_len,
                        "parallelism": head["parallelism"], "optimizer": a.optimizer, "grad_dtype": a.grad_dtype,
                        "master_weights": head.get("master", "fp32")},
             "tflops_per_gpu": head["tflops_per_gpu"],
             "mfu_dense": round(head["tflops_per_gpu"] / peak_tflops(a.dtype, a.fp32_gemm), 4),
-            "peak_hbm_gib": head["peak_hbm_gib"], "state_gib": head["state_gib"], "finite": head["finite"],
+            "peak_hbm_gib": head["peak_hbm_gib"], "state_gib": head["state_gib"],
             "comm_backend": a.comm, "hip_graph": bool(a.graph), "gemm_variant": a.gemm_variant,
             "tp_allreduce": a.tp_allreduce, "wgrad_stream": head.get("wgrad_stream", False),
             "pair_wgrads": head.get("pair_wgrads", False), "tp_transposed": head.get("tp_transposed", False),

@@ -134,3 +134,15 @@ def test_bench_self_launch_eight_ranks_all_methods():
     assert m["tp"]["comm_sizes"] == {"tp": 8}
     assert m["hybrid"]["parallelism"] == "fsdp4xtp2" and m["hybrid"]["comm_sizes"]["dp_ag"] == 4
     assert all(m[k]["finite"] for k in m)
+
+
+def test_bench_data_note_reports_non_finite():
+    """The JSON ``data`` string is derived from the run's ``finite`` flag: a run whose weights
+    overflowed (e.g. ``--init_scale 0.02`` on the flagship stack) must say NON-FINITE, never "finite data throughout"."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    bad = bench.data_note(0.02, False)
+    assert "NON-FINITE" in bad and "finite data throughout" not in bad
+    good = bench.data_note("fan_in", True, overlap=True)
+    assert "finite data throughout" in good and "NON-FINITE" not in good and "side stream" in good
