@@ -237,6 +237,9 @@ def parse(argv=None):
                    help="diagnostic: create the process group before the N=1 headline (as N>1 runs must)")
     p.add_argument("--force_comm", action="store_true",
                    help="exercise the RCCL DDP/FSDP path of the headline at N=1 (size-1 communicators)")
+    p.add_argument("--zero_copy", action="store_true",
+                   help="with --force_comm (ZeRO-2 headline at N=1): copying size-1 reduce-scatters / all-gathers (a "
+                        "separate gradient shard, an all-gather sink) -- the zero_copy side entry as the headline")
     p.add_argument("--hw_queues", type=int, default=0,
                    help="GPU_MAX_HW_QUEUES for this run (HIP hardware queues per process; 0 = leave HIP's setting, "
                         "default 4).  Set before the first HIP call; self-launched ranks inherit it")
@@ -306,13 +309,16 @@ def destroy_mesh(mesh: Mesh) -> None:
 
 def run_method(a, method: str, n: int, world: int, dev: torch.device, steps: int, warmup: int,
                force_comm: bool, model: ModelConfig, observe_steps: int = 0, headline: bool = False,
-               windows: tuple = (0.0, 0.0, 0), fsdp_alias: bool = True) -> dict:
+               windows: tuple = (0.0, 0.0, 0), fsdp_alias: bool = True, zero_alias: bool = True,
+               min_bpc: int | None = None) -> dict:
     """Build the engine for ``method`` on ``n`` ranks, run ``warmup`` untimed + ``steps`` timed steps (+ the
     observed steps), return the method's record.  Collective over all ranks.
 
     ``windows`` = (min warm-up ms, min timed ms, max timed steps): the side-by-side methods' steady-state windows
     (the headline keeps the driver's exact step counts: (0, 0, 0)).  ``fsdp_alias`` False: FSDP at dp = 1 runs its
-    gather / gradient rings and real (copying) size-1 collectives instead of aliasing the full buffers."""
+    gather / gradient rings and real (copying) size-1 collectives instead of aliasing the full buffers; ``zero_alias``
+    False: ZeRO-2 at dp = 1 with a separate gradient shard and an all-gather sink (copying size-1 collectives).
+    ``min_bpc``: overrides --min_bpc."""
     cpu = dev.type == "cpu"
     dp_mode, dp, tp = mesh_of(method, n, a.tp)
     cfg = TrainConfig(model=model, batch_size=a.batch_size, seq_len=a.seq_len, num_steps=steps, dtype=a.dtype,
@@ -323,9 +329,10 @@ def run_method(a, method: str, n: int, world: int, dev: torch.device, steps: int
                       side_optimizer=a.side_opt if headline else 0, tp_allreduce=a.tp_allreduce,
                       wgrad_layout=a.wgrad_layout,
                       relu_mask=not a.no_relu_mask, gemm_tiles_per_block=a.tpb, fp32_gemm=a.fp32_gemm,
-                      gemm_min_bpc=a.min_bpc, master=a.master, wgrad_stream_max_tpc=a.wgrad_stream_max_tpc,
+                      gemm_min_bpc=a.min_bpc if min_bpc is None else min_bpc, master=a.master, wgrad_stream_max_tpc=a.wgrad_stream_max_tpc,
                       wgrad_stream=a.wgrad_stream and headline and not a.graph,
-                      tp_transposed=os.environ.get("DLLM_TP_TRANSPOSED", "1") != "0", fsdp_alias=fsdp_alias)
+                      tp_transposed=os.environ.get("DLLM_TP_TRANSPOSED", "1") != "0", fsdp_alias=fsdp_alias,
+                      zero_alias=zero_alias)
     mesh = Mesh.build(dp, tp, force=force_comm, comm_backend="torch" if cpu else a.comm,
                       device=None if cpu else dev)
     try:
@@ -601,7 +608,7 @@ def main(argv=None) -> int:
     ffn = a.ffn_dim or (a.mp_ffn_dim if a.method == "tp" else 0)
     model = ModelConfig(model_size=a.model_size, ffn_dim=ffn, layers=a.layers, act=a.act, gated=a.gated)
     head = run_method(a, a.method, n, world, dev, a.steps, a.warmup, a.force_comm, model,
-                      observe_steps=a.observe_steps, headline=True)
+                      observe_steps=a.observe_steps, headline=True, zero_alias=not a.zero_copy)
     head_policy = None
     if not cpu:
         from dllm.ops.gemm import _POLICY
@@ -658,7 +665,8 @@ def main(argv=None) -> int:
             if world == 1:
                 rec["methods_note"] = ("N=1: ddp/zero/fsdp/tp/hybrid run their collective code paths over size-1 "
                                        "communicators, which alias in place and move no data (comm.collectives_noop); "
-                                       "fsdp_copy is FSDP with real copying size-1 gathers / reduce-scatters; tp is the "
+                                       "fsdp_copy / zero_copy are FSDP / ZeRO-2 with real copying size-1 gathers / "
+                                       "reduce-scatters (zero_copy at two GEMM blocks per CU, the N>1 policy); tp is the "
                                        "MP config (hidden 4096, FFN 14336, 1 layer); hybrid is the Llama-3-8B-dims "
                                        "SwiGLU stack (32 layers) on FSDP x TP; side methods are timed on steady-state "
                                        "windows (warmup_ms, timed_ms)")
@@ -711,6 +719,11 @@ def main(argv=None) -> int:
         # N=1: FSDP's size-1 collectives alias the full buffers and move nothing; fsdp_copy runs the dp > 1 ring
         # schedule with real (copying) RCCL gathers / reduce-scatters, so its exposed_ms_diff measures collectives
         methods.insert(methods.index("fsdp") + 1, "fsdp_copy")
+    if world == 1 and "zero" in methods and "zero_copy" not in methods:
+        # N=1 proxy of the N>1 headline schedule: ZeRO-2 with copying size-1 RCCL reduce-scatters
+        # (gradients -> a separate shard) and all-gathers (the updated copy -> a sink), at the N>1 grid policy of two
+        # persistent blocks per CU
+        methods.insert(methods.index("zero") + 1, "zero_copy")
     for m in methods:
         current["m"] = m
         mm = model
@@ -721,10 +734,12 @@ def main(argv=None) -> int:
             mm = ModelConfig(model_size=a.model_size, ffn_dim=a.llama_ffn_dim, layers=a.llama_layers, act="silu",
                              gated=True)
         try:
-            r = run_method(a, "fsdp" if m == "fsdp_copy" else m, n, world, dev, a.method_steps or min(a.steps, 10),
+            base = {"fsdp_copy": "fsdp", "zero_copy": "zero"}.get(m, m)
+            r = run_method(a, base, n, world, dev, a.method_steps or min(a.steps, 10),
                            min(a.warmup, 3), force_comm=(world == 1), model=mm, observe_steps=a.observe_steps,
                            windows=(a.side_warmup_ms, a.side_timed_ms, a.side_max_steps),
-                           fsdp_alias=m != "fsdp_copy")
+                           fsdp_alias=m != "fsdp_copy", zero_alias=m != "zero_copy",
+                           min_bpc=(a.min_bpc or 2) if m == "zero_copy" else None)
         except (ValueError, RuntimeError) as e:
             # a side measurement must not cost the headline line (a config / memory error raises on every
             # rank alike; a hang is cut off by the deadline above)

@@ -65,6 +65,11 @@ int dllm_gemm(int in_dtype, int out_dtype, int layout, int epi, int act, const v
                         epi == EPI_ADAMS_T);
   const bool split_epi = (epi == EPI_SGDS || epi == EPI_ADAMS || epi == EPI_SGDS_T || epi == EPI_ADAMS_T);
   if (opt_epi && layout == L_NT) return -1;
+  // activation epilogues: relu / silu / gelu (the bf16 kernels are instantiated per activation only), in the NT / NN
+  // layouts (TN runs the weight gradients: store or a fused optimizer)
+  if ((epi == EPI_ACT || epi == EPI_DACT || epi == EPI_GLU || epi == EPI_DGLU) &&
+      ((act != ACT_RELU && act != ACT_SILU && act != ACT_GELU) || layout == L_TN))
+    return -1;
   if ((epi == EPI_SGD || epi == EPI_ADAM) && out_dtype != DT_F32) return -1;
   // split master: C = the 16-bit residual plane, aux_out = the bf16 working copy (paired 16-B rows: ld % 8 == 0)
   if (split_epi && (out_dtype != DT_BF16 || in_dtype != DT_BF16 || aux_out == nullptr)) return -1;

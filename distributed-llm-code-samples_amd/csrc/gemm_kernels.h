@@ -42,6 +42,9 @@
 #ifndef DLLM_BPRE
 #define DLLM_BPRE 1  // 8-phase kernel: each K-tile's B-half 0 read one phase early (balanced read segments)
 #endif
+#ifndef DLLM_EPI_SKIP
+#define DLLM_EPI_SKIP 0  // diagnostic only: the 8-phase kernels skip their epilogue (wrong results; prices it)
+#endif
 #ifndef DLLM_F32_256
 #define DLLM_F32_256 1
 #endif
@@ -135,7 +138,10 @@ template <> __device__ __forceinline__ void st1<float>(void* b, long i, float v)
 // between the gate (W1, even blocks) and the up projection (W3, odd blocks); a lane's 4 columns and
 // the matching 4 columns 16 further lie in the SAME lane of the neighbouring n-tile, so the pairs are
 // combined by the caller (see epi_glu_pair).
-template <int EPI, typename OutT>
+template <int ACT> __device__ __forceinline__ float actf(int rt, float x) { return act_fwd(ACT < 0 ? rt : ACT, x); }
+template <int ACT> __device__ __forceinline__ float actg(int rt, float x) { return act_grad(ACT < 0 ? rt : ACT, x); }
+
+template <int EPI, typename OutT, int ACT = -1>
 __device__ __forceinline__ void epi4(const GemmArgs& p, int m, int n, f32x4_t v) {
   const long ci = (long)m * p.ldc + n;
   if constexpr (EPI == EPI_STORE) {
@@ -145,11 +151,11 @@ __device__ __forceinline__ void epi4(const GemmArgs& p, int m, int n, f32x4_t v)
   } else if constexpr (EPI == EPI_ACT) {
     if (p.aux_out) Vec4<OutT>::store(p.aux_out, (long)m * p.ldaux + n, v);
     f32x4_t a;
-    for (int r = 0; r < 4; ++r) a[r] = act_fwd(p.act, v[r]);
+    for (int r = 0; r < 4; ++r) a[r] = actf<ACT>(p.act, v[r]);
     Vec4<OutT>::store(p.C, ci, a);
   } else if constexpr (EPI == EPI_DACT) {
     f32x4_t h = Vec4<OutT>::load(p.aux, (long)m * p.ldaux + n);
-    for (int r = 0; r < 4; ++r) v[r] *= act_grad(p.act, h[r]);
+    for (int r = 0; r < 4; ++r) v[r] *= actg<ACT>(p.act, h[r]);
     Vec4<OutT>::store(p.C, ci, v);
   } else if constexpr (EPI == EPI_SGD) {
     f32x4_t w = Vec4<float>::load(p.C, ci);
@@ -211,7 +217,7 @@ __device__ __forceinline__ void epi4(const GemmArgs& p, int m, int n, f32x4_t v)
 // [g|u] pre-activations (N columns) for the backward.
 // EPI_DGLU: acc = da (N/2 de-interleaved columns, the GEMM runs with N/2), aux = interleaved [g|u];
 // output C is interleaved [dg|du] with N = 2*(GEMM N) columns.
-template <typename OutT>
+template <typename OutT, int ACT = -1>
 __device__ __forceinline__ void epi_glu_pair(const GemmArgs& p, int m, int nc_out, int ng, int nu,
                                              f32x4_t g, f32x4_t u) {
   if (p.aux_out) {
@@ -219,10 +225,10 @@ __device__ __forceinline__ void epi_glu_pair(const GemmArgs& p, int m, int nc_ou
     Vec4<OutT>::store(p.aux_out, (long)m * p.ldaux + nu, u);
   }
   f32x4_t a;
-  for (int r = 0; r < 4; ++r) a[r] = act_fwd(p.act, g[r]) * u[r];
+  for (int r = 0; r < 4; ++r) a[r] = actf<ACT>(p.act, g[r]) * u[r];
   Vec4<OutT>::store(p.C, (long)m * p.ldc + nc_out, a);
 }
-template <typename OutT>
+template <typename OutT, int ACT = -1>
 __device__ __forceinline__ void epi_dglu(const GemmArgs& p, int m, int n_da, f32x4_t da) {
   // n_da indexes the de-interleaved F axis; interleaved column of the gate = (n/16)*32 + n%16
   const int blk = n_da >> 4, off = n_da & 15;
@@ -231,8 +237,8 @@ __device__ __forceinline__ void epi_dglu(const GemmArgs& p, int m, int n_da, f32
   f32x4_t u = Vec4<OutT>::load(p.aux, (long)m * p.ldaux + nu);
   f32x4_t dg, du;
   for (int r = 0; r < 4; ++r) {
-    du[r] = da[r] * act_fwd(p.act, g[r]);
-    dg[r] = da[r] * u[r] * act_grad(p.act, g[r]);
+    du[r] = da[r] * actf<ACT>(p.act, g[r]);
+    dg[r] = da[r] * u[r] * actg<ACT>(p.act, g[r]);
   }
   Vec4<OutT>::store(p.C, (long)m * p.ldc + ng, dg);
   Vec4<OutT>::store(p.C, (long)m * p.ldc + nu, du);
@@ -251,8 +257,6 @@ __device__ __forceinline__ void epi_dglu(const GemmArgs& p, int m, int n_da, f32
 // batch.  ACT >= 0 selects the activation at compile time (no per-element switch: the runtime-switch
 // build of the act epilogue was ~14k instructions, larger than the instruction cache).
 // ----------------------------------------------------------------------------------------------
-template <int ACT> __device__ __forceinline__ float actf(int rt, float x) { return act_fwd(ACT < 0 ? rt : ACT, x); }
-template <int ACT> __device__ __forceinline__ float actg(int rt, float x) { return act_grad(ACT < 0 ? rt : ACT, x); }
 
 template <typename T> struct Raw4;
 template <> struct Raw4<uint16_t> {
@@ -327,11 +331,24 @@ __device__ __forceinline__ uint4 tpair_bf16(uint2 x, uint2 y, int lane) {
 // 256x256 tile (8 waves, wc 0..3), 64 for the 256x128 tile of gemm_bf16_pp (4 waves, wc 0..1).
 // BM = 224 (gemm_8ph_body): the second row half has 3 row fragments per wave, at rows 128 + wr*48 + mt*16; row
 // groups with QM = 1, mt = 3 do not exist (DLLM_OK).
-template <int EPI, typename OutT, int ACT, int QNS = 128, int BM = 256>
+// RBCAP caps the epilogue's row-group batch (the persistent fp32-master SGD kernel: its 8-group batch of master
+// planes on top of the main loop's live state needed 3 scratch dwords; utils/kernel_resources.py)
+template <int EPI, typename OutT, int ACT, int QNS = 128, int BM = 256, int RBCAP = 16>
 __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2][2][4][2], int m0, int n0,
                                              int wr, int wc, int lane, void* Cp) {
   static_assert(BM == 256 || (QNS == 128 && EPI != EPI_GLU && EPI != EPI_DGLU), "224-row tiles: no gated epilogues");
   static_assert(!(epi_tout(EPI) || EPI == EPI_STORE_DT) || (BM == 256 && QNS == 128), "transposed outputs: 256x256");
+  if constexpr (ACT < 0 && (EPI == EPI_ACT || EPI == EPI_DACT || EPI == EPI_GLU || EPI == EPI_DGLU)) {
+    // Runtime activation (the fallback / non-default-variant kernels): branch once per tile into a compile-time body.
+    // A per-element switch inside the unrolled row-group loops made hipcc keep the accumulators in a 512-B scratch
+    // array indexed at run time (every runtime-activation DGLU kernel spilled 528 B; utils/kernel_resources.py).
+    switch (p.act) {
+      case ACT_RELU: epilogue_256<EPI, OutT, ACT_RELU, QNS, BM, RBCAP>(p, acc, m0, n0, wr, wc, lane, Cp); return;
+      case ACT_SILU: epilogue_256<EPI, OutT, ACT_SILU, QNS, BM, RBCAP>(p, acc, m0, n0, wr, wc, lane, Cp); return;
+      case ACT_GELU: epilogue_256<EPI, OutT, ACT_GELU, QNS, BM, RBCAP>(p, acc, m0, n0, wr, wc, lane, Cp); return;
+      default: epilogue_256<EPI, OutT, ACT_NONE, QNS, BM, RBCAP>(p, acc, m0, n0, wr, wc, lane, Cp); return;
+    }
+  }
   constexpr int NWC = QNS / 32;       // waves per tile row
   constexpr int TW = 2 * QNS;         // tile width
   constexpr int MASK_WAVES = 2 * NWC; // waves per tile: the ReLU mask holds 16 B per lane and wave
@@ -346,7 +363,7 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
                      : EPI == EPI_STORE || EPI == EPI_STORE_T || EPI == EPI_STORE_DT ? 4 * WR
                      : EPI == EPI_SGD || EPI == EPI_SGDS || EPI == EPI_SGDS_T ? 8
                      : EPI == EPI_ADAM || EPI == EPI_ADAMS || EPI == EPI_ADAMS_T ? 24 : 0;
-  constexpr int RB = epi_batch(COST);
+  constexpr int RB = epi_batch(COST) < RBCAP ? epi_batch(COST) : RBCAP;
   const int pc = pair_col(lane);
 #define DLLM_M(rg) (m0 + ((rg) >> 3) * 128 + wr * ((BM != 256 && ((rg) >> 3)) ? 48 : 64) + ((rg) & 3) * 16 + (lane & 15))
 #define DLLM_OK(rg) (BM == 256 || ((rg) >> 3) == 0 || ((rg) & 3) != 3)
@@ -956,26 +973,41 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_256(GemmArgs p) {
   }
 
   // epilogue: lane holds C[m0 + wr*128 + mt*16 + (lane&15)][n0 + wc*64 + nt*16 + 4*(lane>>4) + r]
+  auto epilogue = [&](auto act_c) {
+    constexpr int A = decltype(act_c)::value;
 #pragma unroll
-  for (int mt = 0; mt < 8; ++mt) {
-    const int m = m0 + wr * 128 + mt * 16 + (lane & 15);
-    if constexpr (EPI == EPI_GLU) {
-      // gate / up blocks alternate every 16 columns: nt even = gate, nt odd = up (same lane)
+    for (int mt = 0; mt < 8; ++mt) {
+      const int m = m0 + wr * 128 + mt * 16 + (lane & 15);
+      if constexpr (EPI == EPI_GLU) {
+        // gate / up blocks alternate every 16 columns: nt even = gate, nt odd = up (same lane)
 #pragma unroll
-      for (int nt = 0; nt < 4; nt += 2) {
-        const int ng = n0 + wc * 64 + nt * 16 + 4 * (lane >> 4);
-        const int nc_out = (ng >> 5) * 16 + (ng & 15);
-        epi_glu_pair<OutT>(p, m, nc_out, ng, ng + 16, acc[mt][nt], acc[mt][nt + 1]);
+        for (int nt = 0; nt < 4; nt += 2) {
+          const int ng = n0 + wc * 64 + nt * 16 + 4 * (lane >> 4);
+          const int nc_out = (ng >> 5) * 16 + (ng & 15);
+          epi_glu_pair<OutT, A>(p, m, nc_out, ng, ng + 16, acc[mt][nt], acc[mt][nt + 1]);
+        }
+      } else if constexpr (EPI == EPI_DGLU) {
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+          epi_dglu<OutT, A>(p, m, n0 + wc * 64 + nt * 16 + 4 * (lane >> 4), acc[mt][nt]);
+      } else {
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+          epi4<EPI, OutT, A>(p, m, n0 + wc * 64 + nt * 16 + 4 * (lane >> 4), acc[mt][nt]);
       }
-    } else if constexpr (EPI == EPI_DGLU) {
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-        epi_dglu<OutT>(p, m, n0 + wc * 64 + nt * 16 + 4 * (lane >> 4), acc[mt][nt]);
-    } else {
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-        epi4<EPI, OutT>(p, m, n0 + wc * 64 + nt * 16 + 4 * (lane >> 4), acc[mt][nt]);
     }
+  };
+  // activation epilogues: one branch per tile into a compile-time activation (a per-element switch kept the
+  // accumulators in scratch, utils/kernel_resources.py)
+  if constexpr (EPI == EPI_ACT || EPI == EPI_DACT || EPI == EPI_GLU || EPI == EPI_DGLU) {
+    switch (p.act) {
+      case ACT_RELU: epilogue(std::integral_constant<int, ACT_RELU>{}); break;
+      case ACT_SILU: epilogue(std::integral_constant<int, ACT_SILU>{}); break;
+      case ACT_GELU: epilogue(std::integral_constant<int, ACT_GELU>{}); break;
+      default: epilogue(std::integral_constant<int, ACT_NONE>{}); break;
+    }
+  } else {
+    epilogue(std::integral_constant<int, -1>{});
   }
 }
 
@@ -1159,12 +1191,17 @@ __device__ __forceinline__ void gemm_8ph_body(const GemmArgs& p, const int which
   // epilogue of a slot; split-K slices write fp32 partial planes C + split*M*ldc
   auto slot_epilogue = [&](int s, f32x4_t (&ac)[2][2][4][2]) {
     const GemmArgs q = reload_args(which);
+#if DLLM_EPI_SKIP
+    // diagnostic build (scripts/bench_epilogue_cost.py): no epilogue -- the accumulators stay live through a branch
+    // the host never takes (beta is 0 or 1 on every launch), so the main loop is unchanged and the results are wrong
+    if (q.beta != 12345.f) return;
+#endif
     int sp, tm0, tn0;
     tile_of(q, s, sp, tm0, tn0);
     void* out = q.C;
     if constexpr (EPI == EPI_STORE)
       if (q.ksplit > 1) out = (char*)q.C + (long)sp * q.M * q.ldc * sizeof(OutT);
-    epilogue_256<EPI, OutT, ACT, 128, BM>(q, ac, tm0, tn0, wr, wc, lane, out);
+    epilogue_256<EPI, OutT, ACT, 128, BM, (PERS && EPI == EPI_SGD) ? 2 : 16>(q, ac, tm0, tn0, wr, wc, lane, out);
   };
   // next slot of this block (>= total: none)
   int next_slot = total;
@@ -2082,19 +2119,28 @@ static void launch_pp_act(const GemmArgs& a0, hipStream_t s) {
   a.tpb = 1;
   hipLaunchKernelGGL((gemm_bf16_pp<L, E, OutT, ACT>), dim3(nb0), dim3(256), 0, s, a);
 }
+template <int L, int E, typename OutT, int NPH>
+static void launch_8ph_stagger(const GemmArgs& a, int nb, hipStream_t s);
 template <int L, int E, typename OutT>
 static void launch_pp(const GemmArgs& a, hipStream_t s) {
-  constexpr bool fwd = L == L_NT && (E == EPI_ACT || E == EPI_GLU);
-  constexpr bool bwd = L == L_NN && (E == EPI_DACT || E == EPI_DGLU);
-  if constexpr ((fwd || bwd) && std::is_same<OutT, uint16_t>::value) {
+  // every bf16 activation epilogue (NT / NN) on a compile-time activation: the runtime-activation pp kernels kept
+  // their accumulators in scratch (utils/kernel_resources.py)
+  constexpr bool actepi = L != L_TN && (E == EPI_ACT || E == EPI_GLU || E == EPI_DACT || E == EPI_DGLU);
+  if constexpr (actepi && !std::is_same<OutT, uint16_t>::value) {
+    // fp32-output activation epilogues (the bf16x6 fp32 path) stay on the 8-phase kernel: the runtime-activation pp
+    // kernels kept their accumulators in scratch
+    launch_8ph_stagger<L, E, OutT, 8>(a, (a.M / BT_M) * (a.N / BT_N), s);
+    return;
+  } else if constexpr (actepi) {
     switch (a.act) {
       case ACT_RELU: launch_pp_act<L, E, OutT, ACT_RELU>(a, s); return;
       case ACT_SILU: launch_pp_act<L, E, OutT, ACT_SILU>(a, s); return;
       case ACT_GELU: launch_pp_act<L, E, OutT, ACT_GELU>(a, s); return;
-      default: break;
+      default: return;   // unreachable: dllm_gemm rejects other activations (no runtime-activation bf16 kernel)
     }
+  } else {
+    launch_pp_act<L, E, OutT, -1>(a, s);
   }
-  launch_pp_act<L, E, OutT, -1>(a, s);
 }
 
 // main kernel writes partials into the workspace, then the reduction applies the epilogue
@@ -2206,10 +2252,11 @@ static void launch_8ph_stagger(const GemmArgs& a, int nb, hipStream_t s) {
       case ACT_RELU: launch_8ph_act<L, E, OutT, ACT_RELU, NPH>(a, nb, s); return;
       case ACT_SILU: launch_8ph_act<L, E, OutT, ACT_SILU, NPH>(a, nb, s); return;
       case ACT_GELU: launch_8ph_act<L, E, OutT, ACT_GELU, NPH>(a, nb, s); return;
-      default: break;
+      default: return;   // unreachable: dllm_gemm rejects other activations (no runtime-activation bf16 kernel)
     }
+  } else {
+    launch_8ph_act<L, E, OutT, -1, NPH>(a, nb, s);
   }
-  launch_8ph_act<L, E, OutT, -1, NPH>(a, nb, s);
 }
 
 template <int L, int E>
@@ -2272,13 +2319,20 @@ static hipError_t dispatch_epi(int path, int epi, const GemmArgs& a, int in_dt, 
     if (path == 1) return launch_f32<L, E>(a, s);                   \
     if (path == 3) return launch_m224<L, E>(a, out_dt, s);          \
     return launch_generic<L, E>(a, in_dt, out_dt, s);
-  switch (epi) {
-    DLLM_EPI_CASE(EPI_STORE)
-    DLLM_EPI_CASE(EPI_ACT)
-    DLLM_EPI_CASE(EPI_DACT)
-    DLLM_EPI_CASE(EPI_GLU)
-    DLLM_EPI_CASE(EPI_DGLU)
-    default: return hipErrorInvalidValue;
+  if constexpr (L == L_TN) {   // weight gradients: store (fused optimizers: dispatch_opt); no activation epilogues
+    switch (epi) {
+      DLLM_EPI_CASE(EPI_STORE)
+      default: return hipErrorInvalidValue;
+    }
+  } else {
+    switch (epi) {
+      DLLM_EPI_CASE(EPI_STORE)
+      DLLM_EPI_CASE(EPI_ACT)
+      DLLM_EPI_CASE(EPI_DACT)
+      DLLM_EPI_CASE(EPI_GLU)
+      DLLM_EPI_CASE(EPI_DGLU)
+      default: return hipErrorInvalidValue;
+    }
   }
 #undef DLLM_EPI_CASE
 }

@@ -119,7 +119,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_pp(GemmArgs p) {
     void* out = q.C;
     if constexpr (EPI == EPI_STORE)
       if (q.ksplit > 1) out = (char*)q.C + (long)sp * q.M * q.ldc * sizeof(OutT);
-    epilogue_256<EPI, OutT, ACT, 64>(q, ac, tm0, tn0, wr, wc, lane, out);
+    epilogue_256<EPI, OutT, ACT, 64, 256, (ACT < 0 ? 2 : 16)>(q, ac, tm0, tn0, wr, wc, lane, out);
   };
 
   // K-tile bases: the current slot's panels, and the next slot's (K-tiles >= nk); without a next slot, K-tiles >= nk

@@ -304,6 +304,9 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str, out: torch.Tensor | None
         raise ValueError(f"epilogue {epi} needs aux (pre-activation)")
     if epi == "glu" and N % 32:
         raise ValueError("gated GEMM needs N % 32 == 0 (16-row interleave)")
+    if epi in ("act", "dact", "glu", "dglu") and a.device.type == "cuda" and (layout == "tn" or act == "none"):
+        # the native library has activation kernels per activation, in the NT / NN layouts only
+        raise ValueError(f"epilogue {epi} on the GPU: relu / silu / gelu in the NT / NN layouts (got {act}, {layout})")
     # fused optimizers: the weight-gradient layouts -- TN, NN on 224-row tiles (transposed-activation TP layout), or
     # the NN weight-gradient layout's 256x256 tiles (split masters)
     opt_layout_ok = layout == "tn" or (layout == "nn" and a.device.type == "cuda" and (

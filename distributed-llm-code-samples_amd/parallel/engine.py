@@ -118,6 +118,23 @@ def gpu_chunk_count(T: int, D: int, F_loc: int, R1: int, c: int) -> int:
     return c
 
 
+def wgrad_nn_shape_problem(T: int, D: int, F_loc: int, R1: int) -> str:
+    """Why the NN weight-gradient layout cannot run at these shapes ('' = it can).  Every GEMM of the layout must sit
+    on the 256x256 8-phase tiles, unsplit: the two weight gradients (dW2 [D, F] and dW1ᵀ [D, R1], K = T) and the two
+    GEMMs whose epilogues write the transposed copies -- fwd-2 (y = a·W2ᵀ: M = T, N = D, K = F) and dx (M = T, N = D,
+    K = R1).  E.g. T = 4224 (33 x 128 rows) passes the weight-gradient checks but not the copies' (T % 256)."""
+    from ..ops.gemm import choose_ksplit, nn_wgrad_supported
+
+    if T % 64 or not all(nn_wgrad_supported(*s) for s in ((D, F_loc, T), (D, R1, T), (T, D, F_loc), (T, D, R1))):
+        return f"shapes (D={D}, F={F_loc}, T={T}) off the 256x256 8-phase tiles"
+    if choose_ksplit(D, F_loc, T) > 1 or choose_ksplit(R1, D, T) > 1 or choose_ksplit(T, D, F_loc) > 1 \
+            or choose_ksplit(T, D, R1) > 1:
+        # small tile grids: the TN weight gradients / the fwd-2 and dx stores run split-K, which the transposed outputs
+        # and copies do not (a different summation order: results would stop matching the TN layout's)
+        return f"small tile grids (T={T}, D={D}, F={F_loc}) take split-K"
+    return ""
+
+
 class FFNTrainer:
     def __init__(self, cfg: TrainConfig, mesh: Mesh, device: torch.device):
         self.cfg, self.mesh, self.device = cfg, mesh, torch.device(device)
@@ -253,6 +270,21 @@ class FFNTrainer:
                                        (cfg.w2_storage == "auto" and self.wgrad_nn and mode == "nn_w2t"))
         if self.w2s and (self.tp_comm or self.sp or self.pair_wgrads):
             raise ValueError("w2_storage transposed: row-major data-parallel / single-device layers only")
+        if self.w2s and dev.type == "cuda":
+            # dW2 is written through the transposed output map on the GPU (any weight-gradient layout): the kernels
+            # that have one -- bf16 operands on unsplit 256x256 tiles, and a fused optimizer on split masters only
+            # (the transposed epilogues are 'store', 'sgd_split', 'adam_split').  Checked here, not at the first backward
+            from ..ops.gemm import choose_ksplit, nn_wgrad_supported
+
+            bad = []
+            if self.cd != torch.bfloat16:
+                bad.append("bf16 compute")
+            if self.fused_opt and not self.split:
+                bad.append("split masters with a fused optimizer")
+            if not nn_wgrad_supported(D, self.F_loc, T) or choose_ksplit(D, self.F_loc, T) > 1:
+                bad.append(f"dW2 [{D}, {self.F_loc}] (K = {T}) on unsplit 256x256 tiles")
+            if bad:
+                raise ValueError("w2_storage transposed needs " + ", ".join(bad))
         self.w2t = self.tmode or self.w2s
 
         # ---- flat owned parameter layout (completion order) ------------------------------------
@@ -448,8 +480,13 @@ class FFNTrainer:
         if self.zero:
             # dp = 1: the owned shard of every bucket is the whole bucket, so the reduced gradient IS the gradient
             # buffer (in-place size-1 reduce-scatter, no copy)
-            self.gshard = (self.grads[:self.shard_total] if d == 1 else
+            # cfg.zero_alias False (bench.py zero_copy): a separate shard and an all-gather sink, so the size-1 RCCL
+            # reduce-scatter / all-gather copy their bytes as the N > 1 collectives do
+            self.zero_alias = d == 1 and cfg.zero_alias
+            self.gshard = (self.grads[:self.shard_total] if self.zero_alias else
                            torch.zeros(self.shard_total, dtype=self.gd, device=dev))
+            self.ag_sink = (torch.empty(self.total, dtype=self.cd, device=dev) if d == 1 and not self.zero_alias
+                            else None)
             self.ag_pending = [None] * len(self.buckets)
             self.rs_issued_at = [None] * len(self.buckets)
         self._next_bucket = 0
@@ -463,7 +500,7 @@ class FFNTrainer:
             raise ValueError(f"unknown wgrad_layout {cfg.wgrad_layout!r}")
         if cfg.wgrad_layout == "tn":
             return False
-        from ..ops.gemm import _VARIANT, BF16_VARIANTS, choose_ksplit, nn_wgrad_supported
+        from ..ops.gemm import _VARIANT, BF16_VARIANTS
 
         T, D = self.T, self.D
         why = []
@@ -475,13 +512,9 @@ class FFNTrainer:
             why.append("kept activations only")
         if self.fused_opt and not self.split:
             why.append("fused optimizer: split masters only")
-        if not (nn_wgrad_supported(D, self.F_loc, T) and nn_wgrad_supported(D, self.R1, T) and T % 64 == 0):
-            why.append(f"shapes (D={D}, F={self.F_loc}, T={T}) off the 256x256 8-phase tiles")
-        elif (choose_ksplit(D, self.F_loc, T) > 1 or choose_ksplit(self.R1, D, T) > 1
-              or choose_ksplit(T, D, self.F_loc) > 1):
-            # small tile grids: the TN weight gradients / the fwd-2 and dx stores run split-K, which the transposed
-            # outputs and copies do not (a different summation order: results would stop matching the TN layout's)
-            why.append(f"small tile grids (T={T}, D={D}, F={self.F_loc}) take split-K")
+        shape_why = wgrad_nn_shape_problem(T, D, self.F_loc, self.R1)
+        if shape_why:
+            why.append(shape_why)
         if BF16_VARIANTS.get(_VARIANT["name"], 0) not in (0, 3):
             why.append(f"GEMM variant {_VARIANT['name']}: transposed outputs run on the 8-phase staggered kernels only")
         if why and cfg.wgrad_layout in ("nn", "nn_w1", "nn_w2t"):
@@ -958,7 +991,8 @@ class FFNTrainer:
         src = self.copy[ss:se]
         if self.device.type != "cuda":
             src = src.clone()  # gloo: keep input and output of the all-gather disjoint
-        self.ag_pending[b] = comm.all_gather_into(self.copy[s_:e_], src, self.mesh.group("dp_ag"), async_op=True)
+        dst = self.copy[s_:e_] if self.ag_sink is None else self.ag_sink[s_:e_]   # sink: dp = 1, zero_alias off
+        self.ag_pending[b] = comm.all_gather_into(dst, src, self.mesh.group("dp_ag"), async_op=True)
         self.rs_issued_at[b] = None
 
     def _ddp_wait(self, l: int, name: str) -> None:

@@ -76,10 +76,11 @@ class TrainConfig:
     # (transposed copies xᵀ / dyᵀ [D, T] from the producing epilogues; models/ffn.NNWgrad), "nn_w1" (dW1 only: xᵀ
     # copies; dW2 stays TN) or "nn_w2t" (nn with W2 stored as W2ᵀ [F, D]: both weight gradients written through the
     # transposed map); "auto" = nn_w2t where the engine supports it (GPU, bf16, 256x256 8-phase shapes without split-K,
-    # no TP / SP / FSDP / recompute, fused SGD / AdamW on split masters or stored gradients)
+    # no TP / SP / recompute, fused SGD / AdamW on split masters or stored gradients; DDP / ZeRO / FSDP meshes included)
     wgrad_layout: str = "auto"
     # W2's storage in the row-major layer: "auto" (transposed W2ᵀ [F, D] with the nn_w2t weight-gradient mode),
-    # "rowmajor", or "transposed" (any weight-gradient layout; no TP / SP / FSDP; checkpoints stay logical [D, F])
+    # "rowmajor", or "transposed" (any weight-gradient layout; no TP / SP / grouped weight-gradient pair; on the GPU bf16
+    # with dW2 on unsplit 256x256 tiles and split masters under a fused optimizer; checkpoints stay logical [D, F])
     w2_storage: str = "auto"
     wgrad_stream: bool = False       # single device, fused optimizer: weight-gradient GEMMs on a second
                                      # stream, concurrent with the dgrad chain (CUs shared; epilogues overlap)
@@ -96,6 +97,10 @@ class TrainConfig:
     force_comm: bool = False         # run the DDP/FSDP collective path even at dp=1 (single-GPU RCCL check)
     fsdp_alias: bool = True          # FSDP at dp = 1: gathers / gradient writes alias the full buffers (size-1
                                      # collectives move nothing); False: the dp > 1 rings + real copying collectives
+    zero_alias: bool = True          # ZeRO-2 at dp = 1: the reduce-scatter output is the gradient buffer itself and
+                                     # the all-gather runs in place (size-1 collectives move nothing); False: a
+                                     # separate gradient shard and an all-gather into a sink buffer -- real copying
+                                     # RCCL collectives, the N > 1 schedule's per-GPU HBM traffic (bench zero_copy)
     force_tp_comm: bool = False      # with force_comm: also run the TP/SP collectives (forward output all-reduce
                                      # in chunks, deferred last-layer all-reduce, dx all-reduce / SP reduce-scatter
                                      # and all-gathers) over the size-1 tp communicator (single-GPU RCCL check)

@@ -22,10 +22,27 @@ def _round_up(n: int, a: int) -> int:
     return (n + a - 1) // a * a
 
 
+def resolve_wgrad_layout(layout: str, D: int, F_loc: int, R1: int, T: int, mode: str = "none", tp: int = 1,
+                         dtype: str = "bf16", recompute: str = "none", sp: bool = False, master: str = "split",
+                         on_gpu: bool = True) -> str:
+    """The weight-gradient layout the engine runs for ``layout`` (mirrors ``FFNTrainer._wgrad_nn_supported``): "auto"
+    -> "nn_w2t" on a GPU in bf16 for row-major data-parallel / single-device layers (no TP / SP, kept activations, a
+    fused optimizer only on split masters) whose GEMMs all sit unsplit on the 256x256 tiles; otherwise "tn"."""
+    if layout != "auto":
+        return layout
+    fused = mode == "none"
+    if not on_gpu or dtype != "bf16" or tp > 1 or sp or recompute != "none" or (fused and master != "split"):
+        return "tn"
+    from ..parallel.engine import wgrad_nn_shape_problem
+
+    return "tn" if wgrad_nn_shape_problem(T, D, F_loc, R1) else "nn_w2t"
+
+
 def plan(D: int, F: int, L: int, tokens: int, dp: int = 1, tp: int = 1, mode: str = "none", gated: bool = False,
          act: str = "relu", dtype: str = "bf16", grad_dtype: str = "bf16", optimizer: str = "sgd",
          recompute: str = "none", relu_mask: bool = True, sequence_parallel: bool = False,
-         align: int = 64, wgrad_stream: bool = False, master: str = "split", wgrad_layout: str = "tn") -> dict:
+         align: int = 64, wgrad_stream: bool = False, master: str = "split", wgrad_layout: str = "auto",
+         on_gpu: bool = True) -> dict:
     """Per-rank bytes by buffer (and GiB totals).  ``mode``: none | ddp | zero | fsdp (over ``dp`` ranks).
     ``wgrad_stream``: the concurrent weight-gradient stream (single device, fused optimizer, kept activations, no
     TP) rotates two dgrad and three dx buffers instead of one and two (``FFNTrainer.da_ring`` / ``dxb``).
@@ -33,7 +50,8 @@ def plan(D: int, F: int, L: int, tokens: int, dp: int = 1, tp: int = 1, mode: st
     (``master_residual``, 2 B/param) instead of a separate fp32 buffer (``master_fp32``, 4 B/param).
     ``wgrad_layout`` (the engine's resolved mode, ``FFNTrainer.wgrad_nn`` / ``wgrad_nn_w2``): nn_w1 keeps a transposed
     copy xᵀ [D, T] of every layer input, nn / nn_w2t also dyᵀ copies rotating with the dx buffers plus the top layer's;
-    the NN modes run the backward serially (no weight-gradient stream)."""
+    the NN modes run the backward serially (no weight-gradient stream).  "auto" resolves as the engine does
+    (``resolve_wgrad_layout``): nn_w2t on a GPU wherever the layout runs, else tn."""
     cd = 2 if dtype == "bf16" else 4
     gd = 2 if grad_dtype == "bf16" else 4
     multi = dp > 1
@@ -73,6 +91,8 @@ def plan(D: int, F: int, L: int, tokens: int, dp: int = 1, tp: int = 1, mode: st
         b["preactivations"] = nA * T * R1 * cd
     if relu_mask and act == "relu" and not gated and dtype == "bf16":
         b["relu_masks"] = nA * (T // 256) * (F_loc // 256) * 8192
+    wgrad_layout = resolve_wgrad_layout(wgrad_layout, D, F_loc, R1, T, mode=mode if multi else "none", tp=tp,
+                                        dtype=dtype, recompute=recompute, sp=sp, master=master, on_gpu=on_gpu)
     # the engine runs the stream only while a weight gradient has <= 4 tiles per CU (TrainConfig.wgrad_stream_max_tpc)
     nn = wgrad_layout in ("nn_w1", "nn", "nn_w2t")
     ws = (wgrad_stream and fused and tp == 1 and keep and not sp and not nn
@@ -89,7 +109,8 @@ def plan(D: int, F: int, L: int, tokens: int, dp: int = 1, tp: int = 1, mode: st
     g = 2**30
     return {"bytes": b, "state_gib": round(state / g, 2), "activations_gib": round((tot - state) / g, 2),
             "total_gib": round(tot / g, 2), "headroom_gib": round(HBM_GIB - tot / g, 1),
-            "params_per_rank": total, "params_total": L * ((2 if gated else 1) * F * D + D * F)}
+            "params_per_rank": total, "params_total": L * ((2 if gated else 1) * F * D + D * F),
+            "wgrad_layout": wgrad_layout}
 
 
 def main():
@@ -104,6 +125,8 @@ def main():
     ap.add_argument("--grad_dtype", default="bf16")
     ap.add_argument("--optimizer", default="sgd")
     ap.add_argument("--gpus", type=int, default=8)
+    ap.add_argument("--wgrad_layout", default="auto", choices=["auto", "tn", "nn", "nn_w1", "nn_w2t"],
+                    help="weight-gradient layout (auto: as the engine resolves it)")
     a = ap.parse_args()
     F = a.ffn_dim or 4 * a.model_size
     n = a.gpus
@@ -113,8 +136,9 @@ def main():
         meshes[f"fsdp{n // 2}xtp2"] = (n // 2, 2, "fsdp")
     for name, (dp, tp, mode) in meshes.items():
         r = plan(a.model_size, F, a.layers, a.tokens, dp, tp, mode, a.gated, a.act, a.dtype, a.grad_dtype,
-                 a.optimizer)
-        print(json.dumps({"mesh": name, **{k: v for k, v in r.items() if k != "bytes"}}))
+                 a.optimizer, wgrad_layout=a.wgrad_layout)
+        print(json.dumps({"mesh": name, "wgrad_layout": r["wgrad_layout"],
+                          **{k: v for k, v in r.items() if k not in ("bytes", "wgrad_layout")}}))
 
 
 if __name__ == "__main__":

@@ -146,3 +146,19 @@ def test_bench_data_note_reports_non_finite():
     assert "NON-FINITE" in bad and "finite data throughout" not in bad
     good = bench.data_note("fan_in", True, overlap=True)
     assert "finite data throughout" in good and "NON-FINITE" not in good and "side stream" in good
+
+
+def test_bench_zero_copy_entry_single_rank(free_port):
+    """At N = 1 the side-by-side methods include zero_copy: ZeRO-2 over size-1 communicators whose reduce-scatters and
+    all-gathers copy (separate shard, all-gather sink), at two GEMM blocks per CU -- the N>1 headline's schedule."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "1", "--warmup", "1",
+           "--backend", "gloo", "--model_size", "64", "--layers", "2", "--batch_size", "2", "--seq_len", "16",
+           "--dtype", "fp32", "--methods", "zero", "--method_steps", "1", "--diff_pairs", "0", "--observe_steps", "0",
+           "--side_warmup_ms", "1", "--side_timed_ms", "1"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(PYTHONPATH=ROOT, MASTER_PORT=str(free_port))
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert set(rec["methods"]) == {"zero", "zero_copy"}
+    assert rec["methods"]["zero_copy"]["parallelism"] == "dp1-zero2-forcecomm" and rec["methods"]["zero_copy"]["finite"]

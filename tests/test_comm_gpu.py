@@ -79,14 +79,14 @@ def test_native_abort_error_path(pg):
     assert not mesh.groups
 
 
-def _run(dp_mode, backend, dtype="fp32", opt="sgd", force=True, fsdp_alias=True):
+def _run(dp_mode, backend, dtype="fp32", opt="sgd", force=True, fsdp_alias=True, zero_alias=True):
     D, F, L, T = 256, 1024, 2, 512
     gen = torch.Generator().manual_seed(9)
     layers = [init_ffn_layer(D, F, gen) for _ in range(L)]
     batches = list(reference_mock_data(torch.randint(100_000, (3,), generator=gen), T, D))
     cfg = TrainConfig(model=ModelConfig(D, F, L), batch_size=1, seq_len=T, dtype=dtype, grad_dtype="fp32",
                       lr=1e-2 if opt == "sgd" else 1e-3, optimizer=opt, dp_mode=dp_mode, force_comm=force,
-                      comm_backend=backend, fsdp_alias=fsdp_alias)
+                      comm_backend=backend, fsdp_alias=fsdp_alias, zero_alias=zero_alias)
     dev = torch.device("cuda", 0)
     mesh = Mesh.build(1, 1, force=force, comm_backend=backend, device=dev)
     eng = FFNTrainer(cfg, mesh, dev)
@@ -116,6 +116,18 @@ def test_fsdp_copying_rings_equal_aliased(pg, backend):
     all-gathers and reduce-scatters gives bitwise the aliased schedule's parameters."""
     a = _run("fsdp", backend, dtype="bf16")
     b = _run("fsdp", backend, dtype="bf16", fsdp_alias=False)
+    for g, w in zip(a, b):
+        for k in w:
+            assert torch.equal(g[k], w[k]), k
+
+
+@pytest.mark.parametrize("backend", ["torch", "native"])
+@pytest.mark.parametrize("opt", ["sgd", "adam"])
+def test_zero_copying_collectives_equal_aliased(pg, backend, opt):
+    """bench.py's zero_copy entry: ZeRO-2 at dp = 1 with a separate gradient shard and an all-gather sink (real copying
+    size-1 RCCL reduce-scatters / all-gathers) gives bitwise the aliased schedule's parameters."""
+    a = _run("zero", backend, dtype="bf16", opt=opt)
+    b = _run("zero", backend, dtype="bf16", opt=opt, zero_alias=False)
     for g, w in zip(a, b):
         for k in w:
             assert torch.equal(g[k], w[k]), k

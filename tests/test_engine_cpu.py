@@ -159,3 +159,30 @@ def test_sizing_counts_wgrad_stream_buffers():
         a = plan(64, 256, 2, 128, wgrad_stream=True, **kw, **off)["bytes"]
         b = plan(64, 256, 2, 128, **kw, **off)["bytes"]
         assert a["dgrad_buffer"] == b["dgrad_buffer"] and a["dx_buffers"] == b["dx_buffers"]
+
+
+def test_wgrad_nn_shapes_cover_the_transposed_copies():
+    """the NN weight-gradient layout also needs the fwd-2 / dx GEMMs that write the transposed copies on
+    256x256 tiles.  T = 4224 (33 x 128 tokens) passes the weight-gradient shape checks but not the copies' (T % 256), so
+    'auto' must fall back to TN (engine and sizing alike) instead of raising at the first forward."""
+    from dllm.ops.gemm import nn_wgrad_supported
+    from dllm.parallel.engine import wgrad_nn_shape_problem
+    from dllm.utils.sizing import plan, resolve_wgrad_layout
+
+    assert nn_wgrad_supported(4096, 16384, 4224)            # the weight gradients alone would pass
+    assert wgrad_nn_shape_problem(4224, 4096, 16384, 16384)
+    assert not wgrad_nn_shape_problem(8192, 4096, 16384, 16384)
+    assert resolve_wgrad_layout("auto", 4096, 16384, 16384, 4224) == "tn"
+    assert resolve_wgrad_layout("auto", 4096, 16384, 16384, 8192) == "nn_w2t"
+    assert resolve_wgrad_layout("auto", 4096, 16384, 16384, 8192, tp=2) == "tn"
+    assert resolve_wgrad_layout("auto", 4096, 16384, 16384, 8192, master="fp32") == "tn"           # fused: split only
+    assert resolve_wgrad_layout("auto", 4096, 16384, 16384, 8192, mode="zero", master="fp32") == "nn_w2t"
+    assert "nn_transposed_copies" not in plan(4096, 16384, 8, 4224)["bytes"]
+    assert plan(4096, 16384, 8, 8192)["bytes"]["nn_transposed_copies"] == (8 + 3) * 4096 * 8192 * 2
+
+
+def test_engine_t4224_keeps_tn_layout():
+    """The engine built at T = 4224 (CPU-constructible) resolves 'auto' to the TN layout."""
+    cfg = TrainConfig(model=ModelConfig(256, 1024, 2, "relu", False), batch_size=33, seq_len=128, dtype="bf16")
+    eng = FFNTrainer(cfg, Mesh(), torch.device("cpu"))
+    assert eng.T == 4224 and eng.wgrad_nn is False and eng.w2t is False

@@ -172,3 +172,52 @@ def test_engine_nn_wgrad_layout_bitwise_tn(variant, monkeypatch):
         assert all(torch.equal(bits(a), bits(b)) for a, b in zip(out["tn"][1], out[layout][1])), layout
         assert torch.equal(bits(out["tn"][0]), bits(out[layout][0])), layout
     assert torch.isfinite(out["nn"][0]).all()
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_engine_tn_layout_w2_transposed_storage_bitwise(fused):
+    """W2 stored as W2ᵀ under the TN weight-gradient layout (the TN kernels' transposed output maps,
+    EPI_STORE_T / EPI_SGDS_T) leaves the same logical parameters and outputs, bit for bit, as row-major storage --
+    fused split-master SGD and stored bf16 gradients, 3 layers x 3 steps."""
+    from dllm.models.ffn import init_ffn_params_device
+    from dllm.parallel.engine import FFNTrainer
+    from dllm.parallel.mesh import Mesh
+    from dllm.utils.config import ModelConfig, TrainConfig
+    from dllm.utils.data import DeviceMockData
+
+    dev = torch.device("cuda", 0)
+    m = ModelConfig(model_size=2048, ffn_dim=8192, layers=3, act="relu")
+    out = {}
+    for storage in ("rowmajor", "transposed"):
+        cfg = TrainConfig(model=m, batch_size=1, seq_len=1024, dtype="bf16", grad_dtype="bf16", lr=1e-3,
+                          wgrad_layout="tn", w2_storage=storage, fused_optimizer=fused)
+        eng = FFNTrainer(cfg, Mesh(), dev)
+        assert eng.wgrad_nn is False and eng.w2t == (storage == "transposed")
+        eng.load_full_params(init_ffn_params_device(m.D, m.F, m.layers, 7, dev))
+        data = DeviceMockData(cfg.tokens, m.D, torch.bfloat16, dev)
+        ys = [eng.train_step(*data.fill(i)).clone() for i in range(3)]
+        torch.cuda.synchronize()
+        params = torch.cat([t.reshape(-1) for p in eng.local_params() for t in (p["w1"], p["w2"])])
+        out[storage] = (params, ys)
+    bits = lambda t: t.view(torch.int16 if t.dtype == BF else torch.int32)   # noqa: E731
+    assert all(torch.equal(bits(a), bits(b)) for a, b in zip(out["rowmajor"][1], out["transposed"][1]))
+    assert torch.equal(bits(out["rowmajor"][0]), bits(out["transposed"][0]))
+    assert torch.isfinite(out["rowmajor"][0]).all()
+
+
+def test_engine_w2_transposed_storage_validated_at_construction():
+    """Transposed W2 storage with a fused optimizer on an fp32 master (no transposed 'sgd' epilogue) or off the
+    256x256 tiles is rejected when the engine is built, not at the first backward."""
+    from dllm.parallel.engine import FFNTrainer
+    from dllm.parallel.mesh import Mesh
+    from dllm.utils.config import ModelConfig, TrainConfig
+
+    dev = torch.device("cuda", 0)
+    m = ModelConfig(model_size=2048, ffn_dim=8192, layers=1, act="relu")
+    with pytest.raises(ValueError, match="split masters"):
+        FFNTrainer(TrainConfig(model=m, batch_size=1, seq_len=1024, dtype="bf16", wgrad_layout="tn",
+                               w2_storage="transposed", master="fp32"), Mesh(), dev)
+    small = ModelConfig(model_size=2048, ffn_dim=8192 + 224, layers=1, act="relu")
+    with pytest.raises(ValueError, match="256x256"):
+        FFNTrainer(TrainConfig(model=small, batch_size=1, seq_len=1024, dtype="bf16", wgrad_layout="tn",
+                               w2_storage="transposed"), Mesh(), dev)
