@@ -42,6 +42,14 @@
 #ifndef DLLM_BPRE
 #define DLLM_BPRE 1  // 8-phase kernel: each K-tile's B-half 0 read one phase early (balanced read segments)
 #endif
+#ifndef DLLM_EPI_PF
+#define DLLM_EPI_PF 1  // 8-phase kernels: prefetch the epilogue's load operands (fused-optimizer master / moment planes,
+                       // ReLU dgrad mask, SwiGLU dgrad pre-activations) by counted LDS-DMA during the tile's last
+                       // K-tiles (0 = load them in the epilogue)
+#endif
+#ifndef DLLM_EPI_PF_LEAD
+#define DLLM_EPI_PF_LEAD 8  // at least this many main-loop iterations (2 K-tiles each) of lead for the first prefetch
+#endif
 #ifndef DLLM_EPI_SKIP
 #define DLLM_EPI_SKIP 0  // diagnostic only: the 8-phase kernels skip their epilogue (wrong results; prices it)
 #endif
@@ -1112,6 +1120,20 @@ __device__ __forceinline__ GemmArgs reload_args(int which = 0) {
     __builtin_amdgcn_sched_barrier(0);                    \
   } while (0)
 
+// Epilogue-operand prefetch (DLLM_EPI_PF): 16-B LDS-DMA pieces per wave and tile that touch exactly the bytes the
+// tile's epilogue will load, so those loads hit L2 / MALL instead of paying a chip-wide HBM read burst at the tile
+// boundary.  The split-master optimizers read hi + lo (2 per row group; AdamW also m and v: 4 more), the ReLU dgrad its
+// 16-B mask, the SwiGLU dgrad two 16-B pre-activation pieces per row group.  0: no prefetch.
+template <int EPI, typename OutT, int ACT>
+constexpr int epi_pf_ops() {
+  if constexpr (!DLLM_EPI_PF || !DLLM_BPRE) return 0;
+  else if constexpr (EPI == EPI_SGDS || EPI == EPI_SGDS_T) return 32;
+  else if constexpr (EPI == EPI_ADAMS || EPI == EPI_ADAMS_T) return 96;
+  else if constexpr (EPI == EPI_DACT && ACT == ACT_RELU && std::is_same<OutT, uint16_t>::value) return 1;
+  else if constexpr (EPI == EPI_DGLU && ACT >= 0 && std::is_same<OutT, uint16_t>::value) return 32;
+  else return 0;
+}
+
 // ACT >= 0: activation of the ACT/DACT/GLU/DGLU epilogues fixed at compile time (-1: runtime p.act)
 // NPH = 8: the 8-phase schedule below (one quadrant = 16 MFMAs per wave per barrier interval).
 // NPH = 4: half-tile phases (two quadrants = 32 MFMAs per interval, two half-tiles restaged per phase):
@@ -1127,7 +1149,10 @@ __device__ __forceinline__ void gemm_8ph_body(const GemmArgs& p, const int which
   constexpr int MT1 = BM == BT_M ? 4 : 3;  // row fragments per wave in the second A half
   // slot(op, hh, buf) = ((op*2 + hh)*2 + buf) * 16 KiB: A in [0, 64K), B in [64K, 128K), so every
   // fragment read is base + a 16-bit immediate
-  __shared__ __attribute__((aligned(16))) char smem[8 * HT];
+  // epilogue-operand prefetch: ops per wave per tile (BM = 256 tiles of the 8-phase loop only); their LDS-DMA writes
+  // land in an 8 KiB sink nobody reads (1 KiB per wave)
+  constexpr int PF_OPS = (NPH == 8 && BM == BT_M && !GRP) ? epi_pf_ops<EPI, OutT, ACT>() : 0;
+  __shared__ __attribute__((aligned(16))) char smem[8 * HT + (PF_OPS ? 8192 : 0)];
   DLLM_LDS char* lds = (DLLM_LDS char*)smem;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1227,6 +1252,84 @@ __device__ __forceinline__ void gemm_8ph_body(const GemmArgs& p, const int which
   auto stage = [&](int op, int hh, int kt, int buf) {
     kt = min(kt, nk - 1);
     stage_at(op, hh, op == 0 ? Apf + kt * a_kstep : Bpf + kt * b_kstep, buf);
+  };
+
+  // ---- epilogue-operand prefetch (PF_OPS > 0) ----
+  // Op j of a tile is issued in P1 (j even) / P5 (j odd) of main-loop iteration it0 + j / 2, after that phase's
+  // stage and MFMA cluster, where it0 = nk/2 - max(ceil(PF_OPS / 2), DLLM_EPI_PF_LEAD): the last ops land a few phases before the
+  // epilogue, the first ones at most the lead ahead (they must stay resident in L2 / MALL meanwhile).  Each op makes
+  // the next two counted waits one deeper (P2 / P3 after a P1 op, P6 / P7 after a P5 op), so they still retire
+  // exactly the staged half-tile they did before; the op itself is waited for only by later waits (vmcnt retires in
+  // issue order on gfx950, loads and stores alike -- hipcc's own waitcnt model for this target).
+  int pf_m0 = 0, pf_n0 = 0;   // tile origin of the slot being computed
+  auto pf_begin = [&](const GemmArgs& q) {
+    if constexpr (PF_OPS > 0) {
+      int sp_;
+      tile_of(q, slot, sp_, pf_m0, pf_n0);
+      pf_m0 = __builtin_amdgcn_readfirstlane(pf_m0);
+      pf_n0 = __builtin_amdgcn_readfirstlane(pf_n0);
+    }
+  };
+  constexpr int PF_W = PF_OPS == 0 ? 0 : ((PF_OPS + 1) / 2 > DLLM_EPI_PF_LEAD ? (PF_OPS + 1) / 2 : DLLM_EPI_PF_LEAD);
+  // issue op j (uniform) of the current slot's epilogue operands: the same 16-B per-lane pieces epilogue_256 loads
+  auto pf_issue = [&](int j) {
+    if constexpr (PF_OPS > 0) {
+      const GemmArgs q = reload_args(which);   // loaded here: no argument stays live in SGPRs across the main loop
+      DLLM_LDS char* sink = lds + 8 * HT + wid * 1024;
+      // the lane id through an opaque copy: hipcc would otherwise hoist the per-lane address terms out of the main
+      // loop and keep them live in VGPRs across it (the persistent kernels are at their 256-register budget)
+      int ln = threadIdx.x & 63;
+      asm volatile("" : "+v"(ln));
+      const int pc = pair_col(ln);
+      const void* base;
+      uint32_t voff;   // byte offset from the plane's base (every plane < 4 GiB)
+      if constexpr (EPI == EPI_DACT) {
+        const uint32_t tile = (uint32_t)(pf_m0 / BM) * (uint32_t)(q.N / BT_N) + pf_n0 / BT_N;
+        base = q.mask ? q.mask : q.aux;   // no mask (the bf16 pre-activation path): touch aux, 16x larger, instead
+        voff = (tile * (8 * 64) + (wr * 4 + wc) * 64 + ln) * 16u;
+      } else if constexpr (EPI == EPI_DGLU) {
+        const int rg = j >> 1, nt = j & 1;
+        const int row = pf_m0 + (rg >> 3) * 128 + wr * 64 + (rg & 3) * 16 + (ln & 15);
+        const int colb = pf_n0 + ((rg >> 2) & 1) * 128 + wc * 32;
+        base = q.aux;
+        voff = ((uint32_t)row * (uint32_t)q.ldaux + 2 * colb + 32 * nt + pc) * 2u;
+      } else {
+        constexpr int PER = (EPI == EPI_SGDS || EPI == EPI_SGDS_T) ? 2 : 6;
+        const int rg = j / PER, k = j - rg * PER;
+        int row, colb;
+        if constexpr (epi_tout(EPI)) {
+          row = pf_n0 + ((rg >> 2) & 1) * 128 + wc * 32 + ((rg >> 1) & 1) * 16 + (ln & 15);
+          colb = pf_m0 + (rg >> 3) * 128 + wr * 64 + (rg & 1) * 32;
+        } else {
+          row = pf_m0 + (rg >> 3) * 128 + wr * 64 + (rg & 3) * 16 + (ln & 15);
+          colb = pf_n0 + ((rg >> 2) & 1) * 128 + wc * 32;
+        }
+        if (k == 0) {
+          base = q.aux_out;
+          voff = ((uint32_t)row * (uint32_t)q.ldaux + colb + pc) * 2u;
+        } else if (k == 1) {
+          base = q.C;
+          voff = ((uint32_t)row * (uint32_t)q.ldc + colb + pc) * 2u;
+        } else {
+          base = k < 4 ? q.opt_m : q.opt_v;
+          voff = ((uint32_t)row * (uint32_t)q.ldc + colb + ((k - 2) & 1) * 16 + 4 * (ln >> 4)) * 4u;
+        }
+      }
+      // uniform 64-bit base + 32-bit per-lane offset: the SGPR-base / VGPR-offset addressing form of the stages
+      glds16((const uint16_t*)((const char*)base + voff), sink);
+    }
+  };
+  // P1 (h = 0) / P5 (h = 1) of iteration it: every iteration issues one op, so the counted waits stay static and the
+  // main loop has no branch (a branch there cost 16 VGPRs and made the persistent kernels spill): outside the window the
+  // op index is clamped to the window's first / last op (a re-touch of lines that are, or will be, prefetched anyway)
+  auto pf_at = [&](int it, int h) {
+    if constexpr (PF_OPS > 0) {
+      int j = 2 * (it - (nk / 2 - PF_W)) + h;
+      // opaque to hipcc: it would otherwise split the main loop at the window start into specialised copies
+      asm volatile("" : "+s"(j));
+      j = j < 0 ? 0 : (j >= PF_OPS ? PF_OPS - 1 : j);
+      pf_issue(j);
+    }
   };
 
   // ---- per-lane fragment base addresses (LDS byte addresses) ----
@@ -1436,6 +1539,7 @@ __device__ __forceinline__ void gemm_8ph_body(const GemmArgs& p, const int which
   if constexpr (STAGGER) {
     if (wr == 1) DLLM_BARRIER();
   }
+  pf_begin(p);
 
   for (;;) {  // slots of this block (one pass unless persistent)
   for (int it = 0; it < nk / 2; ++it) {
@@ -1453,6 +1557,18 @@ __device__ __forceinline__ void gemm_8ph_body(const GemmArgs& p, const int which
     // half-tiles left in flight) retires the B0 staged at P6 / P2 before, read at P3 / P7.
 #define DLLM_PHASE_END8()                                           \
   asm volatile("s_waitcnt vmcnt(8)" ::: "memory");                   \
+  DLLM_LDS_WAIT();                                                   \
+  DLLM_BARRIER();
+    // with epilogue-operand prefetch the P2 / P6 and P3 / P7 waits are one deeper: the op issued in P1 / P5 is
+    // younger than the staged half-tile they retire
+#define DLLM_PHASE_END8_PF()                                        \
+  if constexpr (PF_OPS > 0) asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); \
+  else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");              \
+  DLLM_LDS_WAIT();                                                   \
+  DLLM_BARRIER();
+#define DLLM_PHASE_END6_PF()                                        \
+  if constexpr (PF_OPS > 0) asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); \
+  else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");              \
   DLLM_LDS_WAIT();                                                   \
   DLLM_BARRIER();
     // ---- even buffer (K-tile 2it); its B0 is in fb0 ----
@@ -1477,16 +1593,19 @@ __device__ __forceinline__ void gemm_8ph_body(const GemmArgs& p, const int which
     DLLM_PHASE_END(false)
     fin_b(fb1);
     mfma_quad(acc[0][1], fb1, I0{});
+    // an epilogue-operand prefetch op: after P1's stage and before P2's (the same wait accounting as right after the
+    // stage), here where the A fragments are dead until P2's reads (register pressure)
+    pf_at(it, 0);
     DLLM_BARRIER();
     read_a(I1{}, I0{});
     stage_at(1, 0, Bpf, 0);                    // P2: B0 even
-    DLLM_PHASE_END8()
+    DLLM_PHASE_END8_PF()
     fin_a();
     mfma_quad(acc[1][1], fb1, I1{});
     DLLM_BARRIER();
     read_b(I0{}, I1{}, fb1);                   // odd buffer's B0 (retired at P2) -> fb1 (free after q2)
     stage_at(1, 1, Bpf, 0);                    // P3: B1 even
-    DLLM_PHASE_END(true)
+    DLLM_PHASE_END6_PF()
     fin_b(fb1);
     mfma_quad(acc[1][0], fb0, I1{});
     DLLM_BARRIER();
@@ -1502,20 +1621,23 @@ __device__ __forceinline__ void gemm_8ph_body(const GemmArgs& p, const int which
     DLLM_PHASE_END(false)
     fin_b(fb0);
     mfma_quad(acc[0][1], fb0, I0{});
+    pf_at(it, 1);                              // (see P1)
     DLLM_BARRIER();
     read_a(I1{}, I1{});
     stage_at(1, 0, Bpf + b_kstep, 1);          // P6: B0 odd
-    DLLM_PHASE_END8()
+    DLLM_PHASE_END8_PF()
     fin_a();
     mfma_quad(acc[1][1], fb0, I1{});
     DLLM_BARRIER();
     read_b(I0{}, I0{}, fb0);                   // next even B0 (K-tile 2it+2, or the next slot's K-tile 0) -> fb0
     stage_at(1, 1, Bpf + b_kstep, 1);          // P7: B1 odd
-    DLLM_PHASE_END(true)
+    DLLM_PHASE_END6_PF()
     fin_b(fb0);
     mfma_quad(acc[1][0], fb1, I1{});
     DLLM_BARRIER();
 #undef DLLM_PHASE_END8
+#undef DLLM_PHASE_END8_PF
+#undef DLLM_PHASE_END6_PF
 #else
     // ---- even buffer (K-tile 2it) ----
     read_a(I0{}, I0{}); read_b(I0{}, I0{}, fb0);
@@ -1595,6 +1717,7 @@ __device__ __forceinline__ void gemm_8ph_body(const GemmArgs& p, const int which
         for (int d = 0; d < 2; ++d) acc[a][b][c][d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   slot = next_slot;
   begin_tile();
+  if constexpr (PF_OPS > 0) pf_begin(reload_args(which));
   }  // slots
   }  // NPH == 8
   if constexpr (STAGGER) {

@@ -23,13 +23,14 @@ BUILD = os.path.join(PKG, "build")
 
 # production GEMM families: (mangled-name prefix, VGPR+AGPR budget per lane, LDS bytes the schedule assumes or None)
 #   8-phase 256x256 (+ grouped pair, 224-row): 512 threads, __launch_bounds__(512, 2) -> 2 waves per SIMD -> 256
-#   registers of the unified 512-entry file; 8 x 16 KiB half-tile slots = 128 KiB of LDS
+#   registers of the unified 512-entry file; 8 x 16 KiB half-tile slots = 128 KiB of LDS (+ 8 KiB: the epilogue-operand
+#   prefetch sink of the fused-optimizer / ReLU-dgrad / SwiGLU-dgrad instantiations)
 #   256x128 ping-pong: 2 blocks of 4 waves per CU -> 2 waves per SIMD -> 256; 80 KiB each (two fit in 160 KiB)
 FAMILIES = (
-    ("_ZN4dllm13gemm_bf16_8phI", 256, 131072),
-    ("_ZN4dllm18gemm_bf16_8ph_pairI", 256, 131072),
-    ("_ZN4dllm18gemm_bf16_8ph_m224I", 256, 131072),
-    ("_ZN4dllm12gemm_bf16_ppI", 256, 81920),
+    ("_ZN4dllm13gemm_bf16_8phI", 256, (131072, 139264)),
+    ("_ZN4dllm18gemm_bf16_8ph_pairI", 256, (131072, 139264)),
+    ("_ZN4dllm18gemm_bf16_8ph_m224I", 256, (131072,)),
+    ("_ZN4dllm12gemm_bf16_ppI", 256, (81920,)),
     ("_ZN4dllm13gemm_bf16_256I", 256, None),
     ("_ZN4dllm12gemm_f32_256I", 256, None),
     ("_ZN4dllm12gemm_f32_128I", 256, None),
@@ -86,8 +87,8 @@ def violations(recs: list[dict], families=FAMILIES) -> list[str]:
                 used = -(-r["vgpr"] // 8) * 8 + r["agpr"]
                 if used > regs:
                     bad.append(f"{r['name']}: {r['vgpr']} VGPR + {r['agpr']} AGPR > {regs}")
-                if lds is not None and r["lds"] != lds:
-                    bad.append(f"{r['name']}: {r['lds']} B of LDS, the schedule assumes {lds}")
+                if lds is not None and r["lds"] not in lds:
+                    bad.append(f"{r['name']}: {r['lds']} B of LDS, the schedule assumes one of {lds}")
     return bad
 
 

@@ -54,28 +54,29 @@ def cases(T, D, F, g):
         a = torch.empty(T, F, dtype=bf, device="cuda")
         mask = torch.empty(relu_mask_bytes(T, F), dtype=torch.uint8, device="cuda")
         out[("fwd1_nt_act", mult)] = (lambda x=x, w1=w1, a=a, mask=mask:
-                                      gemm(x, w1, "nt", out=a, epi="act", act="relu", mask=mask), 2 * T * Dk * F)
+                                      gemm(x, w1, "nt", out=a, epi="act", act="relu", mask=mask), 2 * T * Dk * F,
+                                      [a, mask])
         # fwd-2: y = a·W2ᵀ with W2ᵀ [F, D] stored (NN), store + transposed copy yᵀ, K = F
         av, w2t = rnd(T, Fk).relu_(), rnd(Fk, D, s=Fk ** -0.5)
         y, yT = torch.empty(T, D, dtype=bf, device="cuda"), torch.empty(D, T, dtype=bf, device="cuda")
         out[("fwd2_nn_store_dt", mult)] = (lambda av=av, w2t=w2t, y=y, yT=yT: gemm(av, w2t, "nn", out=y, aux_t=yT),
-                                           2 * T * Fk * D)
+                                           2 * T * Fk * D, [y, yT])
         # dgrad: da = dy·W2 ⊙ mask (NT on W2ᵀ), K = D
         dy, w2tk = rnd(T, Dk), rnd(F, Dk, s=Dk ** -0.5)
         da = torch.empty(T, F, dtype=bf, device="cuda")
         out[("dgrad_nt_dact", mult)] = (lambda dy=dy, w2tk=w2tk, da=da, mask=mask:
                                         gemm(dy, w2tk, "nt", out=da, epi="dact", act="relu", aux=a, mask=mask),
-                                        2 * T * Dk * F)
+                                        2 * T * Dk * F, [da])
         # weight gradient: dW1ᵀ = xᵀ·da (NN, K = T), written transposed into the split master of W1 [F, D] + SGD
         xT, dak = rnd(D, Tk), rnd(Tk, F, s=0.1)
         hi, lo = split_master((torch.randn(F, D, generator=g) * D ** -0.5).cuda())
         out[("wgrad_nn_t_sgd", mult)] = (lambda xT=xT, dak=dak, hi=hi, lo=lo:
-                                         gemm(xT, dak, "nn", out=lo, epi="sgd_split", lr=1e-9, aux_out=hi, out_t=True),
-                                         2 * D * Tk * F)
+                                         gemm(xT, dak, "nn", out=lo, epi="sgd_split", lr=1e-3, aux_out=hi, out_t=True),
+                                         2 * D * Tk * F, [hi, lo])
         # weight gradient storing a bf16 gradient (the ZeRO / DDP path), same product
         gw = torch.empty(F, D, dtype=bf, device="cuda")
         out[("wgrad_nn_t_store", mult)] = (lambda xT=xT, dak=dak, gw=gw: gemm(xT, dak, "nn", out=gw, out_t=True),
-                                           2 * D * Tk * F)
+                                           2 * D * Tk * F, [gw])
     return out
 
 
@@ -93,11 +94,33 @@ def main():
         libs[os.path.basename(path)] = _native._load()
     os.environ.pop("DLLM_NATIVE_LIB", None)
     cs = cases(T, D, F, torch.Generator().manual_seed(0))
+    # bitwise: every case's outputs from the same starting state on each library (the first is the reference; an
+    # epilogue-skip build is expected to differ).  The fused-SGD case updates its master planes in place: restore them.
+    if len(libs) > 1:
+        ref, same = {}, {}
+        for ln, lib in libs.items():
+            _native._LIB = lib
+            for k, (fn, _, outs) in cs.items():
+                if k[1] != 1:
+                    continue
+                saved = [t.clone() for t in outs]
+                fn()
+                torch.cuda.synchronize()
+                got = [t.clone() for t in outs]
+                for t, sv in zip(outs, saved):
+                    t.copy_(sv)
+                if ln == "base":
+                    ref[k] = got
+                else:
+                    same[f"{ln}:{k[0]}"] = all(torch.equal(g_.view(torch.uint8), r_.view(torch.uint8))
+                                               for g_, r_ in zip(got, ref[k]))
+        _native._LIB = libs["base"]
+        print("bitwise vs base:", json.dumps(same), flush=True)
     res = {(ln, k): [] for ln in libs for k in cs}
     for _ in range(a.rounds):
         for ln, lib in libs.items():
             _native._LIB = lib
-            for k, (fn, _) in cs.items():
+            for k, (fn, _, _) in cs.items():
                 res[(ln, k)].append(timeit(fn, a.iters))
     _native._LIB = libs["base"]
     table = {}

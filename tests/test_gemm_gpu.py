@@ -239,6 +239,8 @@ def test_fp32_256_epilogues(epi, fp32_mode):
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("epi", ["store", "act", "dact"])
 def test_generic_odd_shapes(layout, dtype, epi):
+    if layout == "tn" and epi != "store":
+        pytest.skip("activation epilogues: NT / NN only (TN runs the weight gradients)")
     M, N, K = 100, 70, 37
     a, b = _operands(layout, M, N, K, dtype, seed=7)
     aux = _mk((M, N), dtype, 9) if epi == "dact" else None
