@@ -43,9 +43,10 @@
 #define DLLM_BPRE 1  // 8-phase kernel: each K-tile's B-half 0 read one phase early (balanced read segments)
 #endif
 #ifndef DLLM_EPI_PF
-#define DLLM_EPI_PF 1  // 8-phase kernels: prefetch the epilogue's load operands (fused-optimizer master / moment planes,
-                       // ReLU dgrad mask, SwiGLU dgrad pre-activations) by counted LDS-DMA during the tile's last
-                       // K-tiles (0 = load them in the epilogue)
+#define DLLM_EPI_PF 0  // 1: 8-phase kernels prefetch the epilogue's load operands (fused-optimizer master / moment planes,
+                       // ReLU dgrad mask, SwiGLU dgrad pre-activations) by counted LDS-DMA in every main-loop iteration.
+                       // Bitwise equal, spill-free -- and slower: the main loop pays more than the epilogue saves
+                       // (fused-SGD weight gradient 855 vs 770 us, step 36.2 vs 34.5 ms; profiles/r6/epilogue_prefetch_r6.txt)
 #endif
 #ifndef DLLM_EPI_PF_LEAD
 #define DLLM_EPI_PF_LEAD 8  // at least this many main-loop iterations (2 K-tiles each) of lead for the first prefetch
