@@ -191,6 +191,9 @@ def parse(argv=None):
                    help="weight-gradient GEMM layout: nn = transposed xᵀ / dyᵀ copies written by the producing "
                         "epilogues, both weight gradients as NN GEMMs with a K-contiguous A (models/ffn.NNWgrad); "
                         "auto = nn wherever the engine supports it")
+    p.add_argument("--w2_storage", choices=["auto", "rowmajor", "transposed"], default="auto",
+                   help="W2 storage in the row-major layer: auto = W2ᵀ with the NN weight-gradient layout and on TP layers "
+                        "(the dgrad then runs NT), rowmajor = [D, F] everywhere")
     p.add_argument("--tp_allreduce", choices=["rccl", "custom", "auto"], default="rccl",
                    help="TP activation all-reduce: RCCL, the custom two-shot xGMI peer all-reduce (csrc/car.hip), or auto "
                         "(both timed on the [T, D] message at engine build on the real tp group, the faster kept; "
@@ -327,7 +330,7 @@ def run_method(a, method: str, n: int, world: int, dev: torch.device, steps: int
                       data="device", force_comm=force_comm, comm_backend=a.comm,
                       force_tp_comm=force_comm and method in ("tp", "hybrid"),
                       side_optimizer=a.side_opt if headline else 0, tp_allreduce=a.tp_allreduce,
-                      wgrad_layout=a.wgrad_layout,
+                      wgrad_layout=a.wgrad_layout, w2_storage=a.w2_storage,
                       relu_mask=not a.no_relu_mask, gemm_tiles_per_block=a.tpb, fp32_gemm=a.fp32_gemm,
                       gemm_min_bpc=a.min_bpc if min_bpc is None else min_bpc, master=a.master, wgrad_stream_max_tpc=a.wgrad_stream_max_tpc,
                       wgrad_stream=a.wgrad_stream and headline and not a.graph,
@@ -470,7 +473,7 @@ def _run_on_mesh(a, method, cfg, mesh, n, world, dev, steps, warmup, force_comm,
            "wgrad_stream": eng.wg_stream is not None,
            # small-grid weight gradients in one grouped launch / F-major activations on 224-row tiles (MP at tp 8)
            "pair_wgrads": bool(eng.pair_wgrads), "tp_transposed": bool(eng.tmode),
-           "wgrad_nn": bool(eng.wgrad_nn), "wgrad_nn_w2": bool(eng.wgrad_nn_w2),
+           "wgrad_nn": bool(eng.wgrad_nn), "wgrad_nn_w2": bool(eng.wgrad_nn_w2), "w2_transposed": bool(eng.w2s),
            # the ranks each role communicator actually spans (RCCL / gloo group sizes; {} = no collective)
            "comm_sizes": {role: g.size() for role, g in mesh.groups.items() if g is not None}}
     if eng.tp_ar_choice is not None:
@@ -554,7 +557,7 @@ def data_note(init, finite: bool, overlap: bool = False) -> str:
 
 SIDE_KEYS = ("value", "ms_per_step", "tflops_per_gpu", "peak_hbm_gib", "parallelism", "model", "global_batch",
              "steps", "warmup", "warmup_ms", "timed_ms", "finite", "init", "state_gib", "comm", "queues", "comm_sizes",
-             "pair_wgrads", "tp_transposed", "wgrad_nn", "wgrad_nn_w2", "tp_allreduce_choice")
+             "pair_wgrads", "tp_transposed", "wgrad_nn", "wgrad_nn_w2", "w2_transposed", "tp_allreduce_choice")
 
 
 def main(argv=None) -> int:
@@ -652,6 +655,7 @@ def main(argv=None) -> int:
             "tp_allreduce": a.tp_allreduce, "wgrad_stream": head.get("wgrad_stream", False),
             "pair_wgrads": head.get("pair_wgrads", False), "tp_transposed": head.get("tp_transposed", False),
             "wgrad_nn": head.get("wgrad_nn", False), "wgrad_nn_w2": head.get("wgrad_nn_w2", False),
+            "w2_transposed": head.get("w2_transposed", False),
         }
         if head_policy is not None:
             rec["gemm_policy"] = head_policy   # raster bands, tiles per block, blocks per CU of the headline's GEMMs

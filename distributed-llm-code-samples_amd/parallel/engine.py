@@ -266,10 +266,14 @@ class FFNTrainer:
         # storage, e.g. ZeRO-sharded checkpoints).  self.w2t: W2ᵀ storage in either layer form (tmode stores it too)
         if cfg.w2_storage not in ("auto", "rowmajor", "transposed"):
             raise ValueError(f"unknown w2_storage {cfg.w2_storage!r}")
-        self.w2s = not self.tmode and (cfg.w2_storage == "transposed" or
-                                       (cfg.w2_storage == "auto" and self.wgrad_nn and mode == "nn_w2t"))
-        if self.w2s and (self.tp_comm or self.sp or self.pair_wgrads):
-            raise ValueError("w2_storage transposed: row-major data-parallel / single-device layers only")
+        # auto: W2ᵀ with the nn_w2t weight-gradient mode, and on row-major TP layers (round 6), where the NN layout does
+        # not run (its transposed copies would be of partial sums) but W2ᵀ storage still turns the dgrad da = dy·W2 into
+        # an NT GEMM (both operands K-contiguous): config 5's SwiGLU dgrad 859 -> 700 us (NN -> NT), fwd-2 NT -> NN,
+        # dW2 through the TN kernels' transposed output map (profiles/r6/config5_hybrid_phases_r6.txt)
+        self.w2s = not self.tmode and (cfg.w2_storage == "transposed" or (cfg.w2_storage == "auto" and (
+            (self.wgrad_nn and mode == "nn_w2t") or self._w2t_for_tp_layers())))
+        if self.w2s and self.pair_wgrads:
+            raise ValueError("w2_storage transposed: not with grouped weight-gradient pairs (they keep W2 row-major)")
         if self.w2s and dev.type == "cuda":
             # dW2 is written through the transposed output map on the GPU (any weight-gradient layout): the kernels
             # that have one -- bf16 operands on unsplit 256x256 tiles, and a fused optimizer on split masters only
@@ -490,6 +494,18 @@ class FFNTrainer:
             self.ag_pending = [None] * len(self.buckets)
             self.rs_issued_at = [None] * len(self.buckets)
         self._next_bucket = 0
+
+    def _w2t_for_tp_layers(self) -> bool:
+        """``w2_storage='auto'`` on row-major TP layers: W2 stored as W2ᵀ when the GPU kernels that then run exist -- bf16,
+        dW2 [D, F/tp] on unsplit 256x256 tiles (the TN transposed output map), split masters under a fused optimizer,
+        no grouped weight-gradient pair."""
+        if not (self.tp_comm and self.device.type == "cuda" and self.cd == torch.bfloat16 and not self.pair_wgrads):
+            return False
+        if self.fused_opt and not self.split:
+            return False
+        from ..ops.gemm import choose_ksplit, nn_wgrad_supported
+
+        return nn_wgrad_supported(self.D, self.F_loc, self.T) and choose_ksplit(self.D, self.F_loc, self.T) == 1
 
     def _wgrad_nn_supported(self) -> bool:
         """Whether the weight gradients run in the NN layout (``cfg.wgrad_layout``; models/ffn.NNWgrad): GPU, bf16, the
@@ -1291,7 +1307,7 @@ class FFNTrainer:
                 hooks_sp = _SPHooks(self, l)
                 dxp = layer_bwd(self.dyfull, xin, w1, w2, act, gated, a, h, gw1, gw2, self.da,
                                 self.dxb[l % 2] if need_dx else None, hooks_sp, mask=self._mask(l),
-                                dx_first=cfg.tp_overlap, pair_wgrads=self.pair_wgrads)
+                                dx_first=cfg.tp_overlap, pair_wgrads=self.pair_wgrads, w2t=self.w2s)
                 if dxp is not None:
                     for w in hooks_sp.rs_work or ():
                         w.wait()
@@ -1398,7 +1414,7 @@ class FFNTrainer:
             gathers[i].wait()
             r = slice(i * rf, (i + 1) * rf)
             layer_fwd(xin[r], w1, w2, self.act, self.gated, a[r], h[r] if h is not None else None, yf,
-                      mask=mask[i * mband:(i + 1) * mband] if mask is not None else None)
+                      mask=mask[i * mband:(i + 1) * mband] if mask is not None else None, w2t=self.w2s)
             pend.append(comm.reduce_scatter_into(yl, yf, tpg, async_op=True))
         self._tp_pending = pend
 
@@ -1419,7 +1435,7 @@ class FFNTrainer:
                 prev[ci].wait()
             layer_fwd(x[r], w1, w2, self.act, self.gated, a[r], h[r] if h is not None else None, y[r],
                       before_fwd2=before2 if ci == 0 else None,
-                      mask=mask[ci * mband:(ci + 1) * mband] if mask is not None else None)
+                      mask=mask[ci * mband:(ci + 1) * mband] if mask is not None else None, w2t=self.w2s)
             if self.tp_car is not None:
                 works.append(self.tp_car.all_reduce_async(y[r]))
             else:

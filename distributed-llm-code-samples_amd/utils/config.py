@@ -78,8 +78,9 @@ class TrainConfig:
     # transposed map); "auto" = nn_w2t where the engine supports it (GPU, bf16, 256x256 8-phase shapes without split-K,
     # no TP / SP / recompute, fused SGD / AdamW on split masters or stored gradients; DDP / ZeRO / FSDP meshes included)
     wgrad_layout: str = "auto"
-    # W2's storage in the row-major layer: "auto" (transposed W2ᵀ [F, D] with the nn_w2t weight-gradient mode),
-    # "rowmajor", or "transposed" (any weight-gradient layout; no TP / SP / grouped weight-gradient pair; on the GPU bf16
+    # W2's storage in the row-major layer: "auto" (transposed W2ᵀ [F, D] with the nn_w2t weight-gradient mode and on
+    # row-major TP layers on the GPU, where it turns the dgrad into an NT GEMM),
+    # "rowmajor", or "transposed" (any weight-gradient layout and mesh but the grouped weight-gradient pair; on the GPU bf16
     # with dW2 on unsplit 256x256 tiles and split masters under a fused optimizer; checkpoints stay logical [D, F])
     w2_storage: str = "auto"
     wgrad_stream: bool = False       # single device, fused optimizer: weight-gradient GEMMs on a second

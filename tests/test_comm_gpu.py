@@ -241,3 +241,32 @@ def test_fsdp_side_stream_priority_bitwise(pg, monkeypatch):
         outs.append(eng.master.clone())
         mesh.destroy()
     assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
+
+
+@pytest.mark.parametrize("gated", [False, True])
+def test_tp_layers_w2_transposed_storage_bitwise(pg, gated):
+    """Round 6: on row-major TP layers W2 is stored as W2ᵀ by default (``w2_storage='auto'``: the dgrad runs NT, fwd-2
+    NN, dW2 through the TN kernels' transposed output map).  FSDP x TP over size-1 RCCL communicators (bench.py's
+    hybrid entry at N=1), 2 steps: bitwise the row-major storage's parameters."""
+    from dllm.models.ffn import init_ffn_params_device
+    from dllm.utils.data import DeviceMockData
+
+    dev = torch.device("cuda", 0)
+    m = ModelConfig(model_size=2048, ffn_dim=8192, layers=2, act="silu" if gated else "relu", gated=gated)
+    out = {}
+    for storage in ("rowmajor", "auto"):
+        cfg = TrainConfig(model=m, batch_size=1, seq_len=1024, dtype="bf16", grad_dtype="bf16", lr=1e-3,
+                          optimizer="adam" if gated else "sgd", dp_mode="fsdp", force_comm=True, force_tp_comm=True,
+                          w2_storage=storage)
+        mesh = Mesh.build(1, 1, force=True, device=dev)
+        eng = FFNTrainer(cfg, mesh, dev)
+        assert eng.tp_comm and eng.fsdp and eng.w2t == (storage == "auto")
+        eng.load_full_params(init_ffn_params_device(m.D, m.F, m.layers, 11, dev, gated=gated))
+        data = DeviceMockData(cfg.tokens, m.D, torch.bfloat16, dev)
+        ys = [eng.train_step(*data.fill(i)).clone() for i in range(2)]
+        torch.cuda.synchronize()
+        out[storage] = (torch.cat([t.reshape(-1) for p in eng.local_params() for t in p.values()]), ys)
+        mesh.destroy()
+    assert all(torch.equal(a.view(torch.int16), b.view(torch.int16)) for a, b in zip(out["rowmajor"][1], out["auto"][1]))
+    assert torch.equal(out["rowmajor"][0].view(torch.int32), out["auto"][0].view(torch.int32))
+    assert torch.isfinite(out["auto"][0]).all()

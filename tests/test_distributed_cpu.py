@@ -329,6 +329,21 @@ def test_w2_transposed_storage_matches_rowmajor(method, n, free_port):
     _close(b["params"], a["params"], rtol=1e-6, atol=1e-8 if n <= 2 else 1e-6)
 
 
+@pytest.mark.parametrize("method,n,extra", [(4, 2, {}), (4, 2, {"sequence_parallel": True}), (5, 4, {}),
+                                            (4, 2, {"tp_chunks": 2})],
+                         ids=["tp2", "tp2_sp", "fsdp2xtp2", "tp2_chunked"])
+def test_w2_transposed_storage_on_tp_layers(method, n, extra, free_port):
+    """Round 6: W2 stored as W2ᵀ on row-major TP layers (the GPU default there: the dgrad runs NT, fwd-2 NN, dW2 through
+    the transposed output map; each TP rank stores W2ᵀ rows F/tp, the column block of W2): the logical parameters
+    equal the row-major run's -- plain TP, sequence parallel, chunked forward, and FSDP x TP."""
+    kw = dict(D=64, F=256, L=3, T=32, steps=4, optimizer="adam", lr=1e-3, **extra)
+    opts = {"tp": 2} if method == 5 else {}
+    a = _run(_cfg(w2_storage="rowmajor", **kw), method, n, free_port, rec=True, **opts)
+    b = _run(_cfg(w2_storage="transposed", **kw), method, n, free_port + 1, rec=True, **opts)
+    assert b["layout"]["w2t"] and not a["layout"]["w2t"]
+    _close(b["params"], a["params"], rtol=1e-6, atol=1e-7)
+
+
 @pytest.mark.parametrize("src,dst", [((3, "transposed"), (6, "rowmajor")), ((6, "transposed"), (3, "transposed")),
                                      ((3, "rowmajor"), (3, "transposed"))], ids=["fsdpT-zero", "zeroT-fsdpT", "fsdp-fsdpT"])
 def test_w2_transposed_storage_fsdp_checkpoints(src, dst, tmp_path, free_port):
