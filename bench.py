@@ -384,6 +384,7 @@ def _run_on_mesh(a, method, cfg, mesh, n, world, dev, steps, warmup, force_comm,
         graphed = GraphedStep(eng, cfg.tokens, model.D)
     else:
         eng.before_backward = data.release
+        data.bind_transposed(*eng.input_transposes())   # the NN layout's xᵀ / dyᵀ drawn with the batch
 
     def one_step(seed):
         old = comm.set_elide(True) if a.elide_collectives else None

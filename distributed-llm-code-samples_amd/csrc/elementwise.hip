@@ -4,6 +4,7 @@
 //                       uniforms, 8 normals per Philox call), 16-B stores.
 //                       Replaces the reference's per-step CPU torch.randn (mock_data, train_ffns.py:144-151;
 //                       ≈430 ms/step on the host at T=8192,D=4096) for throughput mode.
+// * dllm_rng_normal_bf16_t : the bf16 draw of a [R, C] tensor and its transpose in one pass (NN-layout inputs).
 // * dllm_sgd_step     : master -= lr*g (fp32 master, fp32/bf16 grad), refreshes the bf16 working copy.
 //                       Replaces param.add_(-LR*grad) (train_ffns.py:172,259,312) / p-LR*g (:114).
 // * dllm_adam_step    : fused AdamW (north-star optimizer), same flat-buffer contract.
@@ -84,6 +85,53 @@ __global__ __launch_bounds__(256) void rng_normal_bf16_kernel(uint16_t* out, lon
     } else {
       for (int j = 0; j < 8 && base + j < n; ++j) out[base + j] = f2bf(z[j]);
     }
+  }
+}
+
+// rng_normal_bf16_kernel's values for a [R, C] row-major tensor (C % 64 == 0, R % 64 == 0), written both as ``out``
+// [R, C] and as its transpose ``out_t`` [C, R]: the NN weight-gradient layout's xᵀ / dyᵀ of the step's inputs come
+// out of the draw instead of a separate transpose (a 64x64 tile per block: two Philox calls per lane, the 16-B row
+// stores, then the LDS gather and 16-B column stores of transpose_bf16_kernel).  Philox counter of the 8 elements at
+// (r, c..c+7) is (r*C + c)/8, as in the flat kernel, so both outputs are bitwise the flat draw + transpose.
+__global__ __launch_bounds__(256) void rng_normal_bf16_t_kernel(uint16_t* __restrict__ out, long C,
+                                                                uint16_t* __restrict__ out_t, long R, uint64_t seed,
+                                                                uint64_t offset, float scale,
+                                                                const unsigned long long* seed_dev) {
+  __shared__ uint32_t sh[64 * 33];
+  if (seed_dev) seed = *seed_dev;
+  const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
+  const int t = threadIdx.x;
+  const long r0 = (long)blockIdx.y * 64, c0 = (long)blockIdx.x * 64;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int row = t / 8 + 32 * k, ch = t % 8;
+    const long e = (r0 + row) * C + c0 + 8 * ch, i = e / 8;
+    const uint4 ctr = make_uint4((uint32_t)i, (uint32_t)(i >> 32), (uint32_t)offset, (uint32_t)(offset >> 32));
+    const uint4 r = philox4x32_10(ctr, key);
+    float z[8];
+    box_muller16(r.x & 0xffffu, r.x >> 16, scale, z[0], z[1]);
+    box_muller16(r.y & 0xffffu, r.y >> 16, scale, z[2], z[3]);
+    box_muller16(r.z & 0xffffu, r.z >> 16, scale, z[4], z[5]);
+    box_muller16(r.w & 0xffffu, r.w >> 16, scale, z[6], z[7]);
+    uint4 u;
+    u.x = (uint32_t)f2bf(z[0]) | ((uint32_t)f2bf(z[1]) << 16);
+    u.y = (uint32_t)f2bf(z[2]) | ((uint32_t)f2bf(z[3]) << 16);
+    u.z = (uint32_t)f2bf(z[4]) | ((uint32_t)f2bf(z[5]) << 16);
+    u.w = (uint32_t)f2bf(z[6]) | ((uint32_t)f2bf(z[7]) << 16);
+    *(uint4*)(out + e) = u;
+    uint32_t* w = sh + row * 33 + 4 * ch;
+    w[0] = u.x; w[1] = u.y; w[2] = u.z; w[3] = u.w;
+  }
+  __syncthreads();
+  const uint16_t* h = (const uint16_t*)sh;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int c = t / 8 + 32 * k, rc = t % 8;
+    uint32_t q[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      q[j] = (uint32_t)h[(8 * rc + 2 * j) * 66 + c] | ((uint32_t)h[(8 * rc + 2 * j + 1) * 66 + c] << 16);
+    *(uint4*)(out_t + (c0 + c) * R + r0 + 8 * rc) = make_uint4(q[0], q[1], q[2], q[3]);
   }
 }
 
@@ -403,6 +451,16 @@ static int rng_launch(void* out, int dtype, long n, unsigned long long seed, uns
 int dllm_rng_normal(void* out, int dtype, long n, unsigned long long seed, unsigned long long offset, float scale,
                     void* stream) {
   return rng_launch(out, dtype, n, seed, offset, scale, nullptr, stream);
+}
+
+// bf16 [R, C] draw (the same values as dllm_rng_normal) plus its transpose [C, R]; R, C multiples of 64, 16-B
+// aligned bases.  seed_dev (nullable) as in dllm_rng_normal_devseed.
+int dllm_rng_normal_bf16_t(void* out, void* out_t, long R, long C, unsigned long long seed,
+                           const unsigned long long* seed_dev, unsigned long long offset, float scale, void* stream) {
+  if (R <= 0 || C <= 0 || R % 64 || C % 64 || R / 64 > 65535 || ((uintptr_t)out | (uintptr_t)out_t) % 16) return -1;
+  hipLaunchKernelGGL(rng_normal_bf16_t_kernel, dim3(C / 64, R / 64), dim3(256), 0, (hipStream_t)stream,
+                     (uint16_t*)out, C, (uint16_t*)out_t, R, (uint64_t)seed, (uint64_t)offset, scale, seed_dev);
+  return (int)hipGetLastError();
 }
 
 // graph-capturable variant: the seed is read from device memory at execution time

@@ -11,17 +11,38 @@ from .. import _native
 STREAM_X, STREAM_DY = 0, 1
 
 
-def rng_normal_(out: torch.Tensor, seed: int, stream_id: int = 0, scale: float = 1.0) -> torch.Tensor:
+def rng_normal_t_supported(out: torch.Tensor) -> bool:
+    """Whether ``rng_normal_(out, ..., out_t=...)`` runs the one-pass draw + transpose kernel on ``out``."""
+    return (out.device.type == "cuda" and out.dtype == torch.bfloat16 and out.dim() == 2 and out.is_contiguous()
+            and out.shape[0] % 64 == 0 and out.shape[1] % 64 == 0 and out.shape[0] // 64 <= 65535)
+
+
+def rng_normal_(out: torch.Tensor, seed: int, stream_id: int = 0, scale: float = 1.0,
+                out_t: torch.Tensor | None = None) -> torch.Tensor:
     """Fill ``out`` with ``scale·N(0,1)``, deterministic in (seed, stream_id, numel) on any device.
 
     GPU: Philox4x32-10 kernel.  CPU: the same Philox stream computed in torch (bitwise-identical
     uniform draws; normals equal up to libm differences), so CPU tests and GPU runs see the same data.
     fp32 outputs take 32-bit uniforms (4 normals per Philox call); bf16 outputs, which keep 8 mantissa bits, take
     16-bit uniforms (8 normals per call, csrc/elementwise.hip ``rng_normal_bf16_kernel``).
+    ``out_t`` ([C, R] for a 2-D ``out`` [R, C]): also write the transpose -- on the GPU in the same pass
+    (``rng_normal_bf16_t_kernel``, bitwise the draw + ``transpose_bf16``) where ``rng_normal_t_supported(out)``.
     """
     if not out.is_contiguous():
         raise ValueError("rng_normal_ needs a contiguous tensor")
     n = out.numel()
+    if out_t is not None:
+        if out.dim() != 2 or tuple(out_t.shape) != (out.shape[1], out.shape[0]) or out_t.dtype != out.dtype:
+            raise ValueError(f"out_t must be [{out.shape[-1]}, {out.shape[0]}] {out.dtype}")
+        if rng_normal_t_supported(out) and out_t.is_contiguous():
+            rc = _native.lib().dllm_rng_normal_bf16_t(out.data_ptr(), out_t.data_ptr(), out.shape[0], out.shape[1],
+                                                      seed & (2**64 - 1), None, stream_id & (2**64 - 1),
+                                                      float(scale), _native.stream_ptr(out.device))
+            _native.check(rc, "dllm_rng_normal_bf16_t")
+            return out
+        rng_normal_(out, seed, stream_id, scale)
+        out_t.copy_(out.t())
+        return out
     if out.device.type == "cuda":
         rc = _native.lib().dllm_rng_normal(out.data_ptr(), _native.dtype_code(out.dtype), n, seed & (2**64 - 1),
                                            stream_id & (2**64 - 1), float(scale), _native.stream_ptr(out.device))

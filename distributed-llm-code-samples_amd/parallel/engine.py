@@ -495,6 +495,13 @@ class FFNTrainer:
             self.rs_issued_at = [None] * len(self.buckets)
         self._next_bucket = 0
 
+    def input_transposes(self) -> tuple[torch.Tensor | None, torch.Tensor | None]:
+        """The buffers a step's ``x`` / ``dy`` are transposed into (NN weight-gradient layout: layer 0's xᵀ, the top
+        layer's dyᵀ; None where not used), for ``DeviceMockData.bind_transposed``."""
+        if not self.wgrad_nn or self.sp:
+            return None, None
+        return self.xT[0], (self.dyT_top if self.wgrad_nn_w2 else None)
+
     def _w2t_for_tp_layers(self) -> bool:
         """``w2_storage='auto'`` on row-major TP layers: W2 stored as W2ᵀ when the GPU kernels that then run exist -- bf16,
         dW2 [D, F/tp] on unsplit 256x256 tiles (the TN transposed output map), split masters under a fused optimizer,
@@ -1171,13 +1178,20 @@ class FFNTrainer:
             # is joined at the end of every step, and x / dy are not rewritten before the next step)
             from ..ops.gemm import transpose_bf16
 
+            # A batch from DeviceMockData.bind_transposed arrives with them already drawn (tag _dllm_t, consumed here)
+            need_dy = self.wgrad_nn_w2 and getattr(dy, "_dllm_t", None) is not self.dyT_top
+            need_x = getattr(x, "_dllm_t", None) is not self.xT[0]
+            for t_ in (x, dy):
+                if getattr(t_, "_dllm_t", None) is not None:
+                    t_._dllm_t = None
             side = self.wg_stream if (self.wg_stream is not None and _TRANSPOSE_ON_SIDE) else None
-            if side is not None:
+            if side is not None and (need_x or need_dy):
                 side.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
-                if self.wgrad_nn_w2:
+                if need_dy:
                     transpose_bf16(dy, self.dyT_top)
-                transpose_bf16(x, self.xT[0])
+                if need_x:
+                    transpose_bf16(x, self.xT[0])
 
         # ---------------- forward ----------------
         mark = self._mark("forward")

@@ -103,6 +103,8 @@ def run_rank(rank: int, world: int, cfg_dict: dict, method: int, backend: str, p
         meta, ckpt_read = load_into(eng, opts["resume"])
         start_step = int(meta["step"])
     data = make_data(cfg.data, cfg.tokens, cfg.model.D, cfg.torch_dtype, device)
+    if hasattr(data, "bind_transposed"):
+        data.bind_transposed(*eng.input_transposes())
     timer = StepTimer(device)
     stop_after = int(opts.get("stop_after") or len(my_seeds))
     done = start_step

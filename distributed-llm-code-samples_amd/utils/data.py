@@ -9,6 +9,8 @@
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ..ops.elementwise import STREAM_DY, STREAM_X, rng_normal_
@@ -48,10 +50,20 @@ class DeviceMockData:
     def prefetch(self, seed: int) -> None:
         return None
 
-    @staticmethod
-    def _draw(x: torch.Tensor, dy: torch.Tensor, seed: int) -> None:
-        rng_normal_(x, seed=int(seed), stream_id=STREAM_X, scale=1.0)
-        rng_normal_(dy, seed=int(seed), stream_id=STREAM_DY, scale=DLOSS_DX_COEF)
+    def bind_transposed(self, x_t: torch.Tensor | None, dy_t: torch.Tensor | None) -> None:
+        """Draw the transposes xᵀ / dyᵀ too, into the engine's buffers (``FFNEngine.input_transposes()``: the NN
+        weight-gradient layout's layer-0 xᵀ and top-layer dyᵀ), in the same pass as the batch
+        (``rng_normal_bf16_t_kernel``).  Each filled tensor is tagged ``_dllm_t`` = its transpose buffer, which the
+        engine's next ``train_step`` takes instead of transposing (and clears).  Synchronous mode only: with the
+        one-deep pipeline the next draw would overwrite a transpose the current step's backward still reads."""
+        off = self.overlap or os.environ.get("DLLM_DRAW_T", "1") == "0"   # DLLM_DRAW_T=0: engine transposes (A/B)
+        self._t = (None, None) if off else (x_t, dy_t)
+
+    def _draw(self, x: torch.Tensor, dy: torch.Tensor, seed: int) -> None:
+        x_t, dy_t = getattr(self, "_t", (None, None))
+        rng_normal_(x, seed=int(seed), stream_id=STREAM_X, scale=1.0, out_t=x_t)
+        rng_normal_(dy, seed=int(seed), stream_id=STREAM_DY, scale=DLOSS_DX_COEF, out_t=dy_t)
+        x._dllm_t, dy._dllm_t = x_t, dy_t
 
     def fill(self, seed: int, next_seed: int | None = None) -> tuple[torch.Tensor, torch.Tensor]:
         if not self.overlap:

@@ -1,14 +1,18 @@
 #!/bin/bash
-# Round 6: W2ᵀ storage on row-major TP layers (auto): numerics (bitwise vs row-major, 2-rank TP / hybrid on one GPU),
-# config 5's FSDP x TP entry and the MP entry with W2ᵀ vs row-major, interleaved.
+# Round 6: W2ᵀ storage on row-major TP layers and the one-pass draw + transpose of the step's inputs: GPU tests,
+# config 5's FSDP x TP entry with W2ᵀ vs row-major (per-kernel profiles), the headline with the fused draw vs the
+# engine's transposes (DLLM_DRAW_T=0), interleaved (profiles/r6/config5_hybrid_phases_r6.txt, fused_draw_r6.txt).
 source scripts/gpu_steps.sh
 T="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
-step t_tpw2 600 $T tests/test_comm_gpu.py -k "w2_transposed" tests/test_multirank_gpu.py
-C5="--ffn_dim 14336 --layers 32 --act silu --gated --methods none --no_reference_init --steps 10 --warmup 3 --phases --method hybrid --force_comm"
-MP="--method tp --ffn_dim 14336 --layers 1 --methods none --no_reference_init --steps 100 --warmup 20 --force_comm"
-for i in 1 2; do
-  step c5h_auto_$i 400 python -u bench.py $C5 --json_out gpurun_out/c5h_auto_$i.json
-  step c5h_row_$i 400 python -u bench.py $C5 --w2_storage rowmajor --json_out gpurun_out/c5h_row_$i.json
-  step mp_auto_$i 200 python -u bench.py $MP --json_out gpurun_out/mp_auto_$i.json
-  step mp_row_$i 200 python -u bench.py $MP --w2_storage rowmajor --json_out gpurun_out/mp_row_$i.json
+step t_new 300 $T tests/test_gemm_gpu.py tests/test_comm_gpu.py -k "rng or device_data or w2_transposed"
+step t_multirank 600 $T tests/test_multirank_gpu.py
+C5="--ffn_dim 14336 --layers 32 --act silu --gated --methods none --no_reference_init --method hybrid --force_comm"
+for w in auto rowmajor; do
+  step prof_c5h_$w 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c5h_$w -o run -- python3 bench.py $C5 --steps 3 --warmup 2 --w2_storage $w
 done
+H="--steps 20 --warmup 5 --methods none --no_reference_init --phases"
+for i in 1 2 3; do
+  step head_drawt_$i 300 python -u bench.py $H --json_out gpurun_out/head_drawt_$i.json
+  step head_engt_$i 300 env DLLM_DRAW_T=0 python -u bench.py $H --json_out gpurun_out/head_engt_$i.json
+done
+step prof_head_drawt 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_head_drawt -o run -- python3 bench.py --steps 5 --warmup 2 --methods none --no_reference_init

@@ -288,6 +288,56 @@ def test_rng_matches_cpu_philox():
     assert abs(f.mean().item()) < 5e-3 and abs(f.std().item() - 1) < 5e-3
 
 
+@pytest.mark.parametrize("R,C", [(8192, 4096), (192, 320), (64, 64)])
+def test_rng_with_transpose_bitwise(R, C):
+    """The one-pass draw + transpose (rng_normal_bf16_t_kernel) is bitwise the flat draw and the transpose kernel."""
+    from dllm.ops.elementwise import rng_normal_
+    from dllm.ops.gemm import transpose_bf16
+
+    a = torch.empty(R, C, device=DEV, dtype=torch.bfloat16)
+    at = torch.full((C, R), 7.0, device=DEV, dtype=torch.bfloat16)
+    rng_normal_(a, seed=5, stream_id=1, scale=0.1, out_t=at)
+    b = torch.empty_like(a)
+    bt = torch.empty_like(at)
+    rng_normal_(b, seed=5, stream_id=1, scale=0.1)
+    transpose_bf16(b, bt)
+    assert torch.equal(a.view(torch.int16), b.view(torch.int16))
+    assert torch.equal(at.view(torch.int16), bt.view(torch.int16))
+    assert torch.equal(at.view(torch.int16), b.t().contiguous().view(torch.int16))
+
+
+def test_device_data_draws_engine_transposes():
+    """DeviceMockData.bind_transposed: the NN layout's layer-0 xᵀ / top dyᵀ come with the batch, the engine skips its
+    transposes (tag consumed), and the step is bitwise the engine-transposed one."""
+    from dllm.models.ffn import init_ffn_params_device
+    from dllm.parallel.engine import FFNTrainer
+    from dllm.parallel.mesh import Mesh
+    from dllm.utils.config import ModelConfig, TrainConfig
+    from dllm.utils.data import DeviceMockData
+
+    dev = torch.device(DEV)
+
+    def run(bind):
+        m = ModelConfig(model_size=512, ffn_dim=1024, layers=2, act="relu")
+        cfg = TrainConfig(model=m, batch_size=2, seq_len=512, dtype="bf16", optimizer="sgd")
+        eng = FFNTrainer(cfg, Mesh(), dev)
+        assert eng.wgrad_nn and eng.input_transposes()[0] is not None
+        eng.load_full_params(init_ffn_params_device(m.D, m.F, m.layers, 0, dev, scale="fan_in"))
+        data = DeviceMockData(cfg.tokens, m.D, torch.bfloat16, dev)
+        if bind:
+            data.bind_transposed(*eng.input_transposes())
+        for s_ in range(3):
+            x, dy = data.fill(s_)
+            assert (getattr(x, "_dllm_t", None) is eng.xT[0]) == bind
+            eng.train_step(x, dy)
+            assert getattr(x, "_dllm_t", None) is None
+        torch.cuda.synchronize()
+        return [t.float().cpu() for layer in eng.gather_full_params() for t in layer.values()]
+
+    for p0, p1 in zip(run(False), run(True)):
+        assert torch.equal(p0, p1)
+
+
 @pytest.mark.parametrize("gdt", [torch.float32, torch.bfloat16])
 def test_optimizers_match_torch(gdt):
     from dllm.ops.elementwise import adam_step_, sgd_step_

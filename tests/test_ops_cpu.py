@@ -1,4 +1,5 @@
 """CPU checks of the op layer (torch reference path) and helpers."""
+import pytest
 import torch
 
 from dllm.models import reference as R
@@ -226,3 +227,16 @@ def test_raster_band_policies_round_trip():
         finally:
             setter(old)
         assert _POLICY[key] == old
+
+
+def test_rng_out_t_fallback_is_the_transpose():
+    """rng_normal_(..., out_t=) off the GPU kernel's domain: the same draw, plus its transpose."""
+    from dllm.ops.elementwise import rng_normal_
+
+    a, at = torch.empty(96, 40, dtype=torch.bfloat16), torch.empty(40, 96, dtype=torch.bfloat16)
+    rng_normal_(a, seed=3, stream_id=1, scale=0.1, out_t=at)
+    b = torch.empty_like(a)
+    rng_normal_(b, seed=3, stream_id=1, scale=0.1)
+    assert torch.equal(a, b) and torch.equal(at, b.t())
+    with pytest.raises(ValueError):
+        rng_normal_(a, seed=3, out_t=torch.empty(96, 40, dtype=torch.bfloat16))
