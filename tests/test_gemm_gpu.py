@@ -318,8 +318,8 @@ def test_device_data_draws_engine_transposes():
     dev = torch.device(DEV)
 
     def run(bind):
-        m = ModelConfig(model_size=512, ffn_dim=1024, layers=2, act="relu")
-        cfg = TrainConfig(model=m, batch_size=2, seq_len=512, dtype="bf16", optimizer="sgd")
+        m = ModelConfig(model_size=2048, ffn_dim=8192, layers=2, act="relu")   # NN-layout shapes (no split-K)
+        cfg = TrainConfig(model=m, batch_size=1, seq_len=1024, dtype="bf16", optimizer="sgd")
         eng = FFNTrainer(cfg, Mesh(), dev)
         assert eng.wgrad_nn and eng.input_transposes()[0] is not None
         eng.load_full_params(init_ffn_params_device(m.D, m.F, m.layers, 0, dev, scale="fan_in"))
@@ -334,7 +334,14 @@ def test_device_data_draws_engine_transposes():
         torch.cuda.synchronize()
         return [t.float().cpu() for layer in eng.gather_full_params() for t in layer.values()]
 
-    for p0, p1 in zip(run(False), run(True)):
+    from dllm.ops.gemm import set_splitk
+
+    old = set_splitk(False)   # T = 1024: the NN layout's shapes without split-K (as in test_gemm_nnwgrad_gpu.py)
+    try:
+        ref, got = run(False), run(True)
+    finally:
+        set_splitk(old)
+    for p0, p1 in zip(ref, got):
         assert torch.equal(p0, p1)
 
 
