@@ -54,12 +54,6 @@
 #ifndef DLLM_EPI_SKIP
 #define DLLM_EPI_SKIP 0  // diagnostic only: the 8-phase kernels skip their epilogue (wrong results; prices it)
 #endif
-// ReLU-mask dgrad (EPI_DACT with the 1-bit mask, 8-phase 256x256): load the tile's 16-B mask word per lane at the
-// start of the tile (4 VGPRs held through the main loop) instead of in the epilogue, where the load sits behind the
-// next slot's K-tile prefetches and inside the chip-wide epilogue burst.  1 = on.
-#ifndef DLLM_MASK_PRE
-#define DLLM_MASK_PRE 1
-#endif
 #ifndef DLLM_F32_256
 #define DLLM_F32_256 1
 #endif
@@ -348,10 +342,9 @@ __device__ __forceinline__ uint4 tpair_bf16(uint2 x, uint2 y, int lane) {
 // groups with QM = 1, mt = 3 do not exist (DLLM_OK).
 // RBCAP caps the epilogue's row-group batch (the persistent fp32-master SGD kernel: its 8-group batch of master
 // planes on top of the main loop's live state needed 3 scratch dwords; utils/kernel_resources.py)
-// mpre (EPI_DACT with a ReLU mask): this lane's mask word, loaded at the start of the tile (DLLM_MASK_PRE)
 template <int EPI, typename OutT, int ACT, int QNS = 128, int BM = 256, int RBCAP = 16>
 __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2][2][4][2], int m0, int n0,
-                                             int wr, int wc, int lane, void* Cp, const uint4* mpre = nullptr) {
+                                             int wr, int wc, int lane, void* Cp) {
   static_assert(BM == 256 || (QNS == 128 && EPI != EPI_GLU && EPI != EPI_DGLU), "224-row tiles: no gated epilogues");
   static_assert(!(epi_tout(EPI) || EPI == EPI_STORE_DT) || (BM == 256 && QNS == 128), "transposed outputs: 256x256");
   if constexpr (ACT < 0 && (EPI == EPI_ACT || EPI == EPI_DACT || EPI == EPI_GLU || EPI == EPI_DGLU)) {
@@ -533,7 +526,7 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4_t (&acc)[2
     if constexpr (ACT == ACT_RELU && BF) {
       if (p.mask) {
         const long tile = (long)(m0 / BM) * (p.N / TW) + n0 / TW;  // BM x TW tiles
-        const uint4 mv = mpre ? *mpre : ((const uint4*)p.mask)[tile * (MASK_WAVES * 64) + (wr * NWC + wc) * 64 + lane];
+        const uint4 mv = ((const uint4*)p.mask)[tile * (MASK_WAVES * 64) + (wr * NWC + wc) * 64 + lane];
         const uint32_t w[4] = {mv.x, mv.y, mv.z, mv.w};
 #pragma unroll
         for (int rg = 0; rg < 16; ++rg) {
@@ -1221,21 +1214,6 @@ __device__ __forceinline__ void gemm_8ph_body(const GemmArgs& p, const int which
     tile_of(q, s, sp, tm0, tn0);
     return (const uint16_t*)q.B + (B_KC ? (long)tn0 * q.ldb : (long)tn0) + (long)sp * nk * b_kstep;
   };
-  // ReLU-mask dgrad: the slot's mask word, loaded when the slot starts (DLLM_MASK_PRE; the epilogue's own index).  The
-  // load is older than every stage of the slot's main loop, so it only deepens the first counted wait by one op.
-  constexpr bool MPRE = DLLM_MASK_PRE && EPI == EPI_DACT && ACT == ACT_RELU && std::is_same<OutT, uint16_t>::value &&
-                        BM == BT_M && NPH == 8 && !GRP;
-  uint4 mreg = make_uint4(0u, 0u, 0u, 0u);
-  auto mask_pre = [&](const GemmArgs& q, int s) {
-    if constexpr (MPRE) {
-      if (q.mask != nullptr) {
-        int sp_, tm0_, tn0_;
-        tile_of(q, s, sp_, tm0_, tn0_);
-        const long tile = (long)(tm0_ / BT_M) * (q.N / BT_N) + tn0_ / BT_N;
-        mreg = ((const uint4*)q.mask)[tile * 512 + wid * 64 + lane];   // 8 waves x 64 lanes x 16 B per tile
-      }
-    }
-  };
   // epilogue of a slot; split-K slices write fp32 partial planes C + split*M*ldc
   auto slot_epilogue = [&](int s, f32x4_t (&ac)[2][2][4][2]) {
     const GemmArgs q = reload_args(which);
@@ -1249,8 +1227,7 @@ __device__ __forceinline__ void gemm_8ph_body(const GemmArgs& p, const int which
     void* out = q.C;
     if constexpr (EPI == EPI_STORE)
       if (q.ksplit > 1) out = (char*)q.C + (long)sp * q.M * q.ldc * sizeof(OutT);
-    epilogue_256<EPI, OutT, ACT, 128, BM, (PERS && EPI == EPI_SGD) ? 2 : 16>(q, ac, tm0, tn0, wr, wc, lane, out,
-                                                                            MPRE ? &mreg : nullptr);
+    epilogue_256<EPI, OutT, ACT, 128, BM, (PERS && EPI == EPI_SGD) ? 2 : 16>(q, ac, tm0, tn0, wr, wc, lane, out);
   };
   // next slot of this block (>= total: none)
   int next_slot = total;
@@ -1564,7 +1541,6 @@ __device__ __forceinline__ void gemm_8ph_body(const GemmArgs& p, const int which
     if (wr == 1) DLLM_BARRIER();
   }
   pf_begin(p);
-  mask_pre(p, slot);
 
   for (;;) {  // slots of this block (one pass unless persistent)
   for (int it = 0; it < nk / 2; ++it) {
@@ -1743,7 +1719,6 @@ __device__ __forceinline__ void gemm_8ph_body(const GemmArgs& p, const int which
   slot = next_slot;
   begin_tile();
   if constexpr (PF_OPS > 0) pf_begin(reload_args(which));
-  if constexpr (MPRE) mask_pre(reload_args(which), slot);
   }  // slots
   }  // NPH == 8
   if constexpr (STAGGER) {
