@@ -39,3 +39,28 @@ def test_size1_inplace_collectives_move_nothing(monkeypatch):
     assert not comm._moves(None, t, t) and comm._moves(None, o, t)
     monkeypatch.setattr(comm, "_group_size", lambda g: 2)
     assert comm._moves(None, t, t)
+
+
+def test_bind_transposed_draws_and_tags_the_transposes(monkeypatch):
+    """bind_transposed: the batch arrives with xᵀ / dyᵀ written into the bound buffers and tagged (the engine's
+    train_step consumes the tag); the overlap pipeline and DLLM_DRAW_T=0 leave the transposes to the engine."""
+    d = DeviceMockData(64, 32, torch.bfloat16, torch.device("cpu"))
+    xt, dyt = torch.empty(32, 64, dtype=torch.bfloat16), torch.empty(32, 64, dtype=torch.bfloat16)
+    d.bind_transposed(xt, dyt)
+    x, dy = d.fill(5)
+    assert x._dllm_t is xt and dy._dllm_t is dyt
+    assert torch.equal(xt, x.t()) and torch.equal(dyt, dy.t())
+    ref_x, ref_dy = DeviceMockData(64, 32, torch.bfloat16, torch.device("cpu")).fill(5)
+    assert torch.equal(x, ref_x) and torch.equal(dy, ref_dy)       # same values as the unbound draw
+    d.bind_transposed(xt, None)
+    x, dy = d.fill(6)
+    assert x._dllm_t is xt and dy._dllm_t is None
+    monkeypatch.setenv("DLLM_DRAW_T", "0")
+    d.bind_transposed(xt, dyt)
+    x, _ = d.fill(7)
+    assert x._dllm_t is None
+    o = DeviceMockData(64, 32, torch.bfloat16, torch.device("cpu"), overlap=True)   # (CPU: overlap is off anyway)
+    monkeypatch.delenv("DLLM_DRAW_T")
+    o.bind_transposed(xt, dyt)
+    x, _ = o.fill(8)
+    assert x._dllm_t is xt
