@@ -44,6 +44,7 @@ def config_from_args(a) -> TrainConfig:
                        optimizer=a.optimizer, lr=a.lr, weight_decay=a.weight_decay,
                        sequence_parallel=a.sequence_parallel, recompute=a.recompute, bucket_mb=a.bucket_mb,
                        data=a.data, comm_backend=a.comm, debug_sync=a.debug_sync, tp_allreduce=a.tp_allreduce, wgrad_layout=a.wgrad_layout,
+                       w2_storage=a.w2_storage,
                        fp32_gemm=a.fp32_gemm, master=a.master)
 
 

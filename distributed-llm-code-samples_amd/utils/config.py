@@ -156,6 +156,8 @@ def add_extended_args(p: argparse.ArgumentParser) -> None:
                    help="TP activation all-reduce: RCCL or the custom two-shot xGMI peer all-reduce")
     p.add_argument("--wgrad_layout", choices=["auto", "tn", "nn", "nn_w1", "nn_w2t"], default="auto",
                    help="weight-gradient GEMM layout (nn: transposed xᵀ / dyᵀ copies from the producing epilogues)")
+    p.add_argument("--w2_storage", choices=["auto", "rowmajor", "transposed"], default="auto",
+                   help="W2 stored row-major [D, F] or as W2ᵀ [F, D] (auto: with nn_w2t and on row-major TP layers)")
     p.add_argument("--nprocs", type=int, default=0, help="ranks to spawn (0 = all visible GPUs)")
     p.add_argument("--dp", type=int, default=0)
     p.add_argument("--tp", type=int, default=0)
