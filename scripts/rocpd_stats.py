@@ -73,6 +73,19 @@ def main():
         un = sum(e_ - s_ for s_, e_ in comm)
         print(f"\ncomm kernels {keys}: union {un / 1e6:.3f} ms, under GEMMs {hid / 1e6:.3f} ms, "
               f"overlap_frac {hid / un if un else float('nan'):.3f}")
+    if a.step_marker and rows:
+        # step period over the trace's last steps: start-to-start, and the idle time before each step's first kernel
+        # (nothing of the previous step still running: a host that cannot keep the queue fed)
+        st = [i for i, r in enumerate(rows) if a.step_marker in r[0]][::2]
+        per, idle = [], []
+        for i0, i1 in list(zip(st[:-1], st[1:]))[-40:]:
+            per.append(rows[i1][1] - rows[i0][1])
+            idle.append(max(0, rows[i1][1] - max(r[2] for r in rows[i0:i1])))
+        if per:
+            per.sort()
+            idle.sort()
+            print(f"\nsteps {len(per)}: period median {per[len(per) // 2] / 1e3:.1f} us (min {per[0] / 1e3:.1f}, max "
+                  f"{per[-1] / 1e3:.1f}); idle before the step median {idle[len(idle) // 2] / 1e3:.1f} us")
     win = []
     if a.step_marker and rows:
         starts = [i for i, r in enumerate(rows) if a.step_marker in r[0]]
