@@ -398,10 +398,36 @@ def _run_on_mesh(a, method, cfg, mesh, n, world, dev, steps, warmup, force_comm,
             if old is not None:
                 comm.set_elide(old)
 
+    queues = None
+
+    def queue_probe():
+        # which streams share the compute stream's hardware queue; probes spin the GPU and synchronise, so this runs
+        # after the FIRST warm-up step (every stream exists and has run), not between the warm-up and the timed steps:
+        # an idle gap there lets the clock drop and the timed window would start cold (TP8 shard: 0.509 vs 0.485 ms)
+        nonlocal queues
+        if not cpu and a.backend == "nccl":
+            # every stream of this method exists and has run by now: measure which share the compute stream's queue
+            from dllm.utils.streams import queue_report
+
+            sync()
+            sides = {"wgrad": eng.wg_stream, "opt": getattr(eng, "opt_stream", None),
+                     "fsdp": getattr(eng, "fsdp_stream", None), "data": getattr(data, "_stream", None)}
+            queues = queue_report(dev, sides)
+            if mesh.groups:
+                # pairwise: role communicators' streams (identified at mesh build) and the side streams; conflicts =
+                # any of them on the compute queue, or the FSDP gather and reduce-scatter on one queue
+                from dllm.utils.streams import role_queue_report
+
+                named = {r: mesh.role_streams.get(r) for r in mesh.groups if mesh.groups[r] is not None}
+                named.update({k: v for k, v in sides.items() if v is not None})
+                queues.update(role_queue_report(dev, named))
+
     min_warm_ms, min_timed_ms, max_steps = windows
     t_w = time.perf_counter()
     for i in range(warmup):
         one_step(seed_base + i)
+        if i == 0:
+            queue_probe()
     nwarm = warmup
     if min_warm_ms > 0 or min_timed_ms > 0:
         # steady-state windows (side methods): warm up on GPU time, not a step count -- the clock ramps over the first
@@ -425,23 +451,8 @@ def _run_on_mesh(a, method, cfg, mesh, n, world, dev, steps, warmup, force_comm,
         steps = max(steps, min(max_steps or steps, int(-(-1.2 * min_timed_ms // max(step_ms, 1e-3)))))
     warm_total_ms = _agree_max((time.perf_counter() - t_w) * 1e3, world, dev) if (min_warm_ms > 0 or min_timed_ms > 0) \
         else (time.perf_counter() - t_w) * 1e3
-    queues = None
-    if not cpu and a.backend == "nccl":
-        # every stream of this method exists and has run by now: measure which share the compute stream's queue
-        from dllm.utils.streams import queue_report
-
-        sync()
-        sides = {"wgrad": eng.wg_stream, "opt": getattr(eng, "opt_stream", None),
-                 "fsdp": getattr(eng, "fsdp_stream", None), "data": getattr(data, "_stream", None)}
-        queues = queue_report(dev, sides)
-        if mesh.groups:
-            # pairwise: role communicators' streams (identified at mesh build) and the side streams; conflicts =
-            # any of them on the compute queue, or the FSDP gather and reduce-scatter on one queue
-            from dllm.utils.streams import role_queue_report
-
-            named = {r: mesh.role_streams.get(r) for r in mesh.groups if mesh.groups[r] is not None}
-            named.update({k: v for k, v in sides.items() if v is not None})
-            queues.update(role_queue_report(dev, named))
+    if warmup == 0:
+        queue_probe()
     if a.phases and headline and not cpu and graphed is None:
         eng.enable_phase_timing(True)
     sync()
