@@ -38,6 +38,8 @@ _SIGS = {
                                c_float, c_float, c_float, c_int, c_void_p]),
     "dllm_rng_normal": (c_int, [c_void_p, c_int, c_long, c_ull, c_ull, c_float, c_void_p]),
     "dllm_rng_normal_devseed": (c_int, [c_void_p, c_int, c_long, c_void_p, c_ull, c_float, c_void_p]),
+    "dllm_rng_normal_bf16_pair": (c_int, [c_void_p, c_void_p, c_long, c_ull, c_void_p, c_ull, c_ull, c_float, c_float,
+                                          c_void_p]),
     "dllm_rng_normal_bf16_t": (c_int, [c_void_p, c_void_p, c_long, c_long, c_ull, c_void_p, c_ull, c_float, c_void_p]),
     "dllm_sgd_step": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_long, c_float, c_float, c_void_p]),
     "dllm_sgd_step_stream": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_long, c_float, c_float, c_int,

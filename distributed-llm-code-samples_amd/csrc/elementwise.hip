@@ -88,6 +88,45 @@ __global__ __launch_bounds__(256) void rng_normal_bf16_kernel(uint16_t* out, lon
   }
 }
 
+// Two bf16 draws of equal size in one launch (the step's x and dy; blockIdx.y picks the tensor), each bitwise the
+// rng_normal_bf16_kernel draw with its own stream offset and scale.  32-bit element-group indices (n / 8 < 2^31, checked
+// by the host) and the partial last group outside the loop: the flat kernel's 64-bit index arithmetic and per-group
+// bounds test are a tenth of its instructions, and the draw is ALU-bound.
+__global__ __launch_bounds__(256) void rng_normal_bf16_pair_kernel(uint16_t* out0, uint16_t* out1, long n,
+                                                                   uint64_t seed, uint64_t off0, uint64_t off1,
+                                                                   float scale0, float scale1,
+                                                                   const unsigned long long* seed_dev) {
+  if (seed_dev) seed = *seed_dev;
+  const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
+  const bool second = blockIdx.y != 0;
+  uint16_t* out = second ? out1 : out0;
+  const uint64_t offset = second ? off1 : off0;
+  const float scale = second ? scale1 : scale0;
+  const uint32_t full = (uint32_t)(n / 8), stride = gridDim.x * blockDim.x;
+  auto draw8 = [&](uint32_t i, float (&z)[8]) {
+    const uint4 r = philox4x32_10(make_uint4(i, 0u, (uint32_t)offset, (uint32_t)(offset >> 32)), key);
+    box_muller16(r.x & 0xffffu, r.x >> 16, scale, z[0], z[1]);
+    box_muller16(r.y & 0xffffu, r.y >> 16, scale, z[2], z[3]);
+    box_muller16(r.z & 0xffffu, r.z >> 16, scale, z[4], z[5]);
+    box_muller16(r.w & 0xffffu, r.w >> 16, scale, z[6], z[7]);
+  };
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < full; i += stride) {
+    float z[8];
+    draw8(i, z);
+    uint4 u;
+    u.x = (uint32_t)f2bf(z[0]) | ((uint32_t)f2bf(z[1]) << 16);
+    u.y = (uint32_t)f2bf(z[2]) | ((uint32_t)f2bf(z[3]) << 16);
+    u.z = (uint32_t)f2bf(z[4]) | ((uint32_t)f2bf(z[5]) << 16);
+    u.w = (uint32_t)f2bf(z[6]) | ((uint32_t)f2bf(z[7]) << 16);
+    *(uint4*)(out + 8 * (long)i) = u;
+  }
+  if ((long)full * 8 < n && blockIdx.x == 0 && threadIdx.x == 0) {
+    float z[8];
+    draw8(full, z);
+    for (long j = 0; (long)full * 8 + j < n; ++j) out[(long)full * 8 + j] = f2bf(z[j]);
+  }
+}
+
 // rng_normal_bf16_kernel's values for a [R, C] row-major tensor (C % 64 == 0, R % 64 == 0), written both as ``out``
 // [R, C] and as its transpose ``out_t`` [C, R]: the NN weight-gradient layout's xᵀ / dyᵀ of the step's inputs come
 // out of the draw instead of a separate transpose (a 64x64 tile per block: two Philox calls per lane, the 16-B row
@@ -460,6 +499,17 @@ int dllm_rng_normal_bf16_t(void* out, void* out_t, long R, long C, unsigned long
   if (R <= 0 || C <= 0 || R % 64 || C % 64 || R / 64 > 65535 || ((uintptr_t)out | (uintptr_t)out_t) % 16) return -1;
   hipLaunchKernelGGL(rng_normal_bf16_t_kernel, dim3(C / 64, R / 64), dim3(256), 0, (hipStream_t)stream,
                      (uint16_t*)out, C, (uint16_t*)out_t, R, (uint64_t)seed, (uint64_t)offset, scale, seed_dev);
+  return (int)hipGetLastError();
+}
+
+// two bf16 tensors of n elements each, in one launch (bitwise two dllm_rng_normal calls); n / 8 < 2^31
+int dllm_rng_normal_bf16_pair(void* out0, void* out1, long n, unsigned long long seed,
+                              const unsigned long long* seed_dev, unsigned long long off0, unsigned long long off1,
+                              float scale0, float scale1, void* stream) {
+  if (n <= 0 || n / 8 >= (1L << 31) || ((uintptr_t)out0 | (uintptr_t)out1) % 16) return -1;
+  hipLaunchKernelGGL(rng_normal_bf16_pair_kernel, dim3(grid_for((n + 7) / 8), 2), dim3(256), 0, (hipStream_t)stream,
+                     (uint16_t*)out0, (uint16_t*)out1, n, (uint64_t)seed, (uint64_t)off0, (uint64_t)off1, scale0,
+                     scale1, seed_dev);
   return (int)hipGetLastError();
 }
 

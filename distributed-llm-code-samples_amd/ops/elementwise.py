@@ -52,6 +52,21 @@ def rng_normal_(out: torch.Tensor, seed: int, stream_id: int = 0, scale: float =
     return out
 
 
+def rng_normal_pair_(a: torch.Tensor, b: torch.Tensor, seed: int, stream_a: int, scale_a: float, stream_b: int,
+                     scale_b: float) -> None:
+    """``rng_normal_(a, seed, stream_a, scale_a)`` and ``rng_normal_(b, seed, stream_b, scale_b)`` -- on the GPU for two
+    contiguous bf16 tensors of one size in a single launch (``rng_normal_bf16_pair_kernel``, bitwise the two draws)."""
+    if (a.device.type == "cuda" and a.dtype == b.dtype == torch.bfloat16 and a.numel() == b.numel() and
+            a.is_contiguous() and b.is_contiguous() and a.device == b.device and a.numel() // 8 < 2**31):
+        rc = _native.lib().dllm_rng_normal_bf16_pair(a.data_ptr(), b.data_ptr(), a.numel(), seed & (2**64 - 1), None,
+                                                     stream_a & (2**64 - 1), stream_b & (2**64 - 1), float(scale_a),
+                                                     float(scale_b), _native.stream_ptr(a.device))
+        _native.check(rc, "dllm_rng_normal_bf16_pair")
+        return
+    rng_normal_(a, seed, stream_a, scale_a)
+    rng_normal_(b, seed, stream_b, scale_b)
+
+
 def rng_normal_devseed_(out: torch.Tensor, seed_dev: torch.Tensor, stream_id: int = 0,
                         scale: float = 1.0) -> torch.Tensor:
     """``rng_normal_`` with the seed read from a 1-element int64 device tensor at execution time, so the

@@ -13,7 +13,7 @@ import os
 
 import torch
 
-from ..ops.elementwise import STREAM_DY, STREAM_X, rng_normal_
+from ..ops.elementwise import STREAM_DY, STREAM_X, rng_normal_, rng_normal_pair_
 from .config import DLOSS_DX_COEF
 
 
@@ -61,8 +61,12 @@ class DeviceMockData:
 
     def _draw(self, x: torch.Tensor, dy: torch.Tensor, seed: int) -> None:
         x_t, dy_t = getattr(self, "_t", (None, None))
-        rng_normal_(x, seed=int(seed), stream_id=STREAM_X, scale=1.0, out_t=x_t)
-        rng_normal_(dy, seed=int(seed), stream_id=STREAM_DY, scale=DLOSS_DX_COEF, out_t=dy_t)
+        if x_t is None and dy_t is None and os.environ.get("DLLM_RNG_PAIR", "1") != "0":
+            # both in one launch on the GPU (rng_normal_bf16_pair_kernel; the same values)
+            rng_normal_pair_(x, dy, int(seed), STREAM_X, 1.0, STREAM_DY, DLOSS_DX_COEF)
+        else:
+            rng_normal_(x, seed=int(seed), stream_id=STREAM_X, scale=1.0, out_t=x_t)
+            rng_normal_(dy, seed=int(seed), stream_id=STREAM_DY, scale=DLOSS_DX_COEF, out_t=dy_t)
         x._dllm_t, dy._dllm_t = x_t, dy_t
 
     def fill(self, seed: int, next_seed: int | None = None) -> tuple[torch.Tensor, torch.Tensor]:

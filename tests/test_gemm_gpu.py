@@ -306,6 +306,20 @@ def test_rng_with_transpose_bitwise(R, C):
     assert torch.equal(at.view(torch.int16), b.t().contiguous().view(torch.int16))
 
 
+@pytest.mark.parametrize("n", [8192 * 1792, 4099, 64])
+def test_rng_pair_bitwise(n):
+    """x and dy in one launch (rng_normal_bf16_pair_kernel) are bitwise the two separate draws, tails included."""
+    from dllm.ops.elementwise import rng_normal_, rng_normal_pair_
+
+    a, b = torch.empty(n, device=DEV, dtype=torch.bfloat16), torch.empty(n, device=DEV, dtype=torch.bfloat16)
+    rng_normal_pair_(a, b, 11, 0, 1.0, 1, 0.1)
+    a1, b1 = torch.empty_like(a), torch.empty_like(b)
+    rng_normal_(a1, seed=11, stream_id=0, scale=1.0)
+    rng_normal_(b1, seed=11, stream_id=1, scale=0.1)
+    assert torch.equal(a.view(torch.int16), a1.view(torch.int16))
+    assert torch.equal(b.view(torch.int16), b1.view(torch.int16))
+
+
 def test_device_data_draws_engine_transposes():
     """DeviceMockData.bind_transposed: the NN layout's layer-0 xᵀ / top dyᵀ come with the batch, the engine skips its
     transposes (tag consumed), and the step is bitwise the engine-transposed one."""
