@@ -52,16 +52,28 @@ def rng_normal_(out: torch.Tensor, seed: int, stream_id: int = 0, scale: float =
     return out
 
 
+def _pair_ok(a: torch.Tensor, b: torch.Tensor) -> bool:
+    return (a.device.type == "cuda" and a.dtype == b.dtype == torch.bfloat16 and a.numel() == b.numel() and
+            a.is_contiguous() and b.is_contiguous() and a.device == b.device and a.numel() // 8 < 2**31)
+
+
 def rng_normal_pair_(a: torch.Tensor, b: torch.Tensor, seed: int, stream_a: int, scale_a: float, stream_b: int,
-                     scale_b: float) -> None:
+                     scale_b: float, seed_dev: torch.Tensor | None = None) -> None:
     """``rng_normal_(a, seed, stream_a, scale_a)`` and ``rng_normal_(b, seed, stream_b, scale_b)`` -- on the GPU for two
-    contiguous bf16 tensors of one size in a single launch (``rng_normal_bf16_pair_kernel``, bitwise the two draws)."""
-    if (a.device.type == "cuda" and a.dtype == b.dtype == torch.bfloat16 and a.numel() == b.numel() and
-            a.is_contiguous() and b.is_contiguous() and a.device == b.device and a.numel() // 8 < 2**31):
-        rc = _native.lib().dllm_rng_normal_bf16_pair(a.data_ptr(), b.data_ptr(), a.numel(), seed & (2**64 - 1), None,
+    contiguous bf16 tensors of one size in a single launch (``rng_normal_bf16_pair_kernel``, bitwise the two draws).
+    ``seed_dev``: read the seed from this 1-element int64 device tensor at execution time (HIP-graph replays)."""
+    if _pair_ok(a, b):
+        if seed_dev is not None and (seed_dev.dtype != torch.int64 or seed_dev.device != a.device):
+            raise TypeError("seed_dev must be an int64 tensor on the outputs' device")
+        rc = _native.lib().dllm_rng_normal_bf16_pair(a.data_ptr(), b.data_ptr(), a.numel(), seed & (2**64 - 1),
+                                                     seed_dev.data_ptr() if seed_dev is not None else None,
                                                      stream_a & (2**64 - 1), stream_b & (2**64 - 1), float(scale_a),
                                                      float(scale_b), _native.stream_ptr(a.device))
         _native.check(rc, "dllm_rng_normal_bf16_pair")
+        return
+    if seed_dev is not None:
+        rng_normal_devseed_(a, seed_dev, stream_a, scale_a)
+        rng_normal_devseed_(b, seed_dev, stream_b, scale_b)
         return
     rng_normal_(a, seed, stream_a, scale_a)
     rng_normal_(b, seed, stream_b, scale_b)

@@ -2,7 +2,7 @@
 
 ``GraphedStep`` captures device mock-data generation + forward + backward + fused optimizer of the
 single-device / TP-free path once, then replays it: one ``hipGraphLaunch`` per step instead of ~60 kernel
-launches through Python.  The per-step data seed lives in device memory (``rng_normal_devseed_``), so each
+launches through Python.  The per-step data seed lives in device memory (``rng_normal_pair_(..., seed_dev=)``), so each
 replay draws new data; everything else is static (preallocated flat buffers, fixed shapes).
 
 Restrictions (checked): no gradient collectives (``eng.fused_opt`` path), SGD (AdamW's bias correction is a
@@ -12,7 +12,7 @@ from __future__ import annotations
 
 import torch
 
-from ..ops.elementwise import STREAM_DY, STREAM_X, rng_normal_devseed_
+from ..ops.elementwise import STREAM_DY, STREAM_X, rng_normal_pair_
 from .config import DLOSS_DX_COEF
 
 
@@ -43,8 +43,7 @@ class GraphedStep:
             self._body()
 
     def _body(self):
-        rng_normal_devseed_(self.x, self.seed, STREAM_X, 1.0)
-        rng_normal_devseed_(self.dy, self.seed, STREAM_DY, DLOSS_DX_COEF)
+        rng_normal_pair_(self.x, self.dy, 0, STREAM_X, 1.0, STREAM_DY, DLOSS_DX_COEF, seed_dev=self.seed)
         self.eng.train_step(self.x, self.dy)
 
     def step(self, seed: int) -> None:
