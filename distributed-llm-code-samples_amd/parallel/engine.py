@@ -47,7 +47,7 @@ import torch
 from ..models.ffn import (NNWgrad, deinterleave_w13, interleave_w13, layer_bwd, layer_bwd_t, layer_fwd, layer_fwd_t,
                           needs_preact, recompute_fwd1, wgrad_w1, wgrad_w2)
 from ..ops.elementwise import adam_split_step_, adam_step_, cast_, sgd_split_step_, sgd_step_
-from ..ops.master import join_flat, part_flat, split_master
+from ..ops.master import join_flat, part_flat
 from ..utils import streams
 from ..utils.config import TrainConfig
 from . import comm
